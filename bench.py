@@ -1,0 +1,254 @@
+#!/usr/bin/env python3
+"""Headline benchmark: cosine top-k queries/sec on MI355X.
+
+Workload (BASELINE.json configs[2], the config its metric is quoted on; it fits
+one GPU): 100,000 queries x 1,000,000 corpus rows x 768 dims, f32, cosine,
+k = 100.  Synthetic N(0,1) f32 embeddings generated on device (torch.randn,
+seeded); inputs are resident in HBM before the timed region.
+
+One step = one full top-k pass of all M queries against the corpus:
+  N = 1: fused GEMM + top-k (libpmm.so, pmm_topk_f32_device) over the corpus.
+  N > 1: the corpus is row-sharded over the ranks (one process per GPU);
+         each rank runs the fused top-k on its shard (global indices via
+         index_base), rank 0 gathers the per-shard M x k lists over RCCL
+         (torch.distributed "nccl" = RCCL) and k-way merges them
+         (pmm_merge_topk_device).  Total work is fixed: "scaling": "strong".
+
+Run: python bench.py [--gpus N] [--steps K] [--warmup W]
+     (N > 1 under torch.distributed.run, one rank per GPU)
+
+Prints ONE JSON line on rank 0 with the metric, the dominant kernel's roofline
+(achieved TFLOP/s from HIP events on its launch stream vs the 157.3 TFLOP/s
+f32 MFMA peak) and a CPU baseline (the oracle, a port of the reference's
+algorithm, on a bounded query sample on this host's cores).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "polars-matmul_amd"), os.path.join(ROOT, "oracle")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+CONFIGS = {
+    # name: (M, N, D, k, metric)
+    "c3": (100_000, 1_000_000, 768, 100, "cosine"),
+    "c2": (1_000, 10_000, 256, 10, "dot"),
+    "c1": (1_000, 10_000, 256, 10, "cosine"),
+}
+F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense FP32 matrix (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def load_traffic(config: str):
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    --pmc summary (profiles/), corrected as MI355X_MICROARCH.md prescribes."""
+    path = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(q_dev, c_dev, k, metric, n_sample, threads):
+    """Time the oracle (reference structure: threaded GEMM, single-threaded
+    epilogue + per-row select) on the first n_sample queries vs the full
+    corpus; returns queries/sec."""
+    import oracle
+
+    q = q_dev[:n_sample].float().cpu().numpy()
+    c = c_dev.float().cpu().numpy()
+    mid = oracle.metric_from_str(metric)
+    t0 = time.perf_counter()
+    oracle.topk(q, c, k, mid, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return n_sample / dt, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-sample", type=int, default=512, help="queries timed on the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 torch top-k")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    from polars_matmul import _native
+
+    _native.check(_native.lib().pmm_set_device(torch.cuda.current_device()))
+
+    M, N, D, k, metric = CONFIGS[args.config]
+    mid = _native.metric_from_str(metric)
+    lo = N * rank // world
+    hi = N * (rank + 1) // world
+    n_loc = hi - lo
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(42)
+    q = torch.randn((M, D), generator=g, device=dev, dtype=torch.float32)
+    g.manual_seed(1_000_003 + rank)
+    c = torch.randn((n_loc, D), generator=g, device=dev, dtype=torch.float32)
+    out_i = torch.empty((M, k), dtype=torch.int32, device=dev)
+    out_s = torch.empty((M, k), dtype=torch.float32, device=dev)
+    ws_bytes = _native.workspace_bytes(M, n_loc, D, k, mid)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    if world > 1 and rank == 0:
+        gath_i = [torch.empty((M, k), dtype=torch.int32, device=dev) for _ in range(world)]
+        gath_s = [torch.empty((M, k), dtype=torch.float32, device=dev) for _ in range(world)]
+        fin_i = torch.empty((M, k), dtype=torch.int32, device=dev)
+        fin_s = torch.empty((M, k), dtype=torch.float32, device=dev)
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        _native.topk_device(q.data_ptr(), D, M, c.data_ptr(), D, n_loc, D, k, mid,
+                            out_i.data_ptr(), out_s.data_ptr(), index_base=lo,
+                            workspace=ws.data_ptr(), workspace_bytes=ws_bytes, stream=stream)
+        if world > 1:
+            dist.gather(out_i, gath_i if rank == 0 else None, dst=0)
+            dist.gather(out_s, gath_s if rank == 0 else None, dst=0)
+            if rank == 0:
+                si = torch.stack(gath_i, dim=1).contiguous()
+                ss = torch.stack(gath_s, dim=1).contiguous()
+                _native.merge_device(si.data_ptr(), ss.data_ptr(), M, world, k, k, mid,
+                                     fin_i.data_ptr(), fin_s.data_ptr(), stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    _native.timing_reset()
+    _native.timing_enable(True)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step()
+        log(f"[rank {rank}] step {i + 1}/{args.steps} issued")
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    _native.timing_enable(False)
+    kern_ms, kern_n = _native.timing_read("gemm_f32_topk")
+    merge_ms, merge_n = _native.timing_read("merge_topk")
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # correctness spot check on a few rows (f64 torch on device; untimed)
+    check = None
+    if args.check and world == 1:
+        rows = torch.arange(0, M, max(1, M // args.check), device=dev)[: args.check]
+        qd = q[rows].double()
+        cd = c.double()
+        s = qd @ cd.T
+        if metric == "cosine":
+            s = s / (qd.norm(dim=1, keepdim=True) * cd.norm(dim=1)[None, :])
+        ref_s, ref_i = torch.topk(s, k, dim=1)
+        got_i = out_i[rows].long()
+        got_s = out_s[rows].double()
+        kth = ref_s[:, -1:]
+        band = 1e-5 * kth.abs() + 1e-5
+        in_set = torch.gather(s, 1, got_i) >= (kth - band)
+        check = {
+            "rows": int(rows.numel()),
+            "valid_topk_frac": float(in_set.float().mean().item()),
+            "exact_index_match_frac": float((got_i == ref_i).float().mean().item()),
+            "max_abs_score_err": float((got_s - torch.gather(s, 1, got_i)).abs().max().item()),
+        }
+        log(f"spot check: {check}")
+
+    if rank != 0:
+        if dist:
+            dist.destroy_process_group()
+        return
+
+    ms_per_step = elapsed / args.steps * 1000.0
+    qps = M * args.steps / elapsed
+    flops_launch = 2.0 * M * n_loc * D
+    avg_kern_s = (kern_ms / kern_n / 1000.0) if kern_n else None
+    achieved = flops_launch / avg_kern_s / 1e12 if avg_kern_s else None
+    roofline = {
+        "bound": "mfma",
+        "kernel": "gemm_f32_kernel<0,cosine> (fused GEMM + top-k)",
+        "achieved": round(achieved, 2) if achieved else None,
+        "peak": F32_MFMA_PEAK_TFLOPS,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+        "traffic": load_traffic(args.config),
+        "kernel_ms_avg": round(kern_ms / kern_n, 3) if kern_n else None,
+        "flops_per_launch": flops_launch,
+        "merge_ms_avg": round(merge_ms / merge_n, 3) if merge_n else None,
+    }
+    cpu = None
+    if args.cpu_sample and world == 1:
+        n_s = min(args.cpu_sample, M)
+        cpu_qps, cpu_dt = cpu_baseline(q, c, k, metric, n_s, args.cpu_threads)
+        cpu = {
+            "value": round(cpu_qps, 2),
+            "unit": "queries/s",
+            "cores": args.cpu_threads,
+            "kind": "port",
+            "sample": f"first {n_s} queries x full {N}-row corpus, {D}d f32 {metric} k={k}; "
+                      f"oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select), {cpu_dt:.1f}s",
+        }
+    line = {
+        "metric": "cosine top-k queries/sec",
+        "value": round(qps, 2),
+        "unit": "queries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic N(0,1) f32 embeddings generated on device (torch.randn, seeded)",
+        "config": {"workload": f"{M}x{N}x{D} f32 {metric} k={k} ({args.config})", "queries": M,
+                   "corpus": N, "dim": D, "k": k, "metric": metric,
+                   "parallelism": f"corpus-row-shard x{world}" if world > 1 else "single GPU"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "check": check,
+    }
+    print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,145 @@
+/*
+ * pmm.h -- C ABI of the MI355X-native similarity-search engine (libpmm.so).
+ *
+ * Drop-in boundary for the reference's `.pmm.topk` / `.pmm.matmul` hot path
+ * (NivekNey/polars-matmul v0.1.4).  The reference binds its Rust numerics to
+ * Python through pyo3 (src/lib.rs:15-62); the numerics themselves are
+ * src/matmul.rs:295-519, src/metrics.rs:38-393 and src/topk.rs:1-75.  Every
+ * entry point below names the reference function it replaces.  Plain pointers
+ * and sizes only: no torch / Arrow / Polars types cross this boundary.
+ *
+ * Conventions
+ *   - Matrices are row-major.  Q is m x d (queries), C is n x d (corpus).
+ *   - Return value: PMM_OK (0) or a PMM_ERR_* code; the message of the last
+ *     failure on the calling thread is available from pmm_last_error().
+ *   - Thread safety: every entry point may be called concurrently from
+ *     different threads (each thread owns its HIP stream and scratch).  The
+ *     reference runs two `.pmm` expressions concurrently inside one Polars
+ *     plan (tests/test_polars_matmul.py:551-572).
+ *   - Result order per query row: best first (descending score for cosine /
+ *     dot, ascending distance for euclidean); equal scores break to the lower
+ *     corpus index; NaN scores rank last.  The reference leaves the order of
+ *     equal scores unspecified (src/topk.rs:55-59, partial_cmp -> Equal).
+ */
+#ifndef PMM_H_
+#define PMM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PMM_OK 0
+#define PMM_ERR_ARG 1         /* invalid argument (sizes, pointers, metric) */
+#define PMM_ERR_HIP 2         /* HIP runtime error (message has the HIP text) */
+#define PMM_ERR_UNSUPPORTED 3 /* combination not supported by this build */
+#define PMM_ERR_NODEVICE 4    /* no gfx950 device visible */
+
+/* Metric ids; src/metrics.rs:10-18 `enum Metric`. */
+#define PMM_METRIC_COSINE 0
+#define PMM_METRIC_DOT 1
+#define PMM_METRIC_EUCLIDEAN 2
+
+/* Arithmetic the top-k GEMM runs in (f32 inputs).  F32 = exact f32 MFMA
+ * (v_mfma_f32_32x32x2_f32), the reference's precision.  BF16 = inputs rounded
+ * to bf16 (RNE) on device, f32 accumulate (v_mfma_f32_32x32x16_bf16); scores
+ * of the returned rows are recomputed exactly in f32. */
+#define PMM_COMPUTE_F32 0
+#define PMM_COMPUTE_BF16 1
+
+const char *pmm_version(void);
+
+/* Message of the last failing call on this thread ("" if none). */
+const char *pmm_last_error(void);
+
+/* Replaces Metric::from_str (src/metrics.rs:20-27): case-insensitive
+ * "cosine" | "dot" | "euclidean" | "l2".  Unknown names return PMM_ERR_ARG with
+ * pmm_last_error() = "Unknown metric: '<s>'. Supported: cosine, dot, euclidean"
+ * (the reference's text, src/metrics.rs:25). */
+int pmm_metric_from_str(const char *s, int *metric);
+
+/* Replaces Metric::higher_is_better (src/metrics.rs:30-35). */
+int pmm_metric_higher_is_better(int metric);
+
+int pmm_device_count(int *count);
+/* Selects the HIP device used by later calls on this thread. */
+int pmm_set_device(int device);
+
+/* ---------------------------------------------------------------------------
+ * Host-buffer entry points (what `_topk` / `_matmul` call; src/lib.rs:15-55).
+ * Inputs are borrowed for the duration of the call and copied to HBM; outputs
+ * are caller-allocated host buffers.
+ * ------------------------------------------------------------------------- */
+
+/* Replaces compute_topk_indices_scores, f32 branch (src/matmul.rs:429-448):
+ * compute_similarity_matrix_f32 (src/metrics.rs:314-365) +
+ * select_topk_with_scores_f32 (src/topk.rs:42-75), fused so the m x n score
+ * matrix is never materialised.  k is clipped to n (src/matmul.rs:443) by the
+ * caller; out_idx / out_score hold m*k entries.  Scores are f32 here; the
+ * Python layer widens them to f64 as src/matmul.rs:447 does. */
+int pmm_topk_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d, int64_t k,
+                 int metric, uint32_t *out_idx, float *out_score);
+
+/* Same with an explicit compute mode (PMM_COMPUTE_F32 / PMM_COMPUTE_BF16). */
+int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_t d, int64_t k,
+                    int metric, int compute, uint32_t *out_idx, float *out_score);
+
+/* Replaces compute_topk_indices_scores, f64 branch (src/matmul.rs:449-468):
+ * compute_similarity_matrix (src/metrics.rs:258-311) +
+ * select_topk_with_scores (src/topk.rs:6-39). */
+int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t d, int64_t k,
+                 int metric, uint32_t *out_idx, double *out_score);
+
+/* Replaces matmul_slice_f32 / matmul_f32 (src/metrics.rs:160-202, :204-255):
+ * out (m x n, row-major) = Q * C^T. */
+int pmm_matmul_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d, float *out);
+
+/* Replaces matmul_slice_f64 / matmul_f64 (src/metrics.rs:111-157, :40-97). */
+int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t d,
+                   double *out);
+
+/* ---------------------------------------------------------------------------
+ * Device-resident entry points: inputs already in HBM, work enqueued on the
+ * caller's HIP stream (NULL = this thread's stream), no host synchronisation.
+ * Used by the benchmark and the multi-GPU (corpus-sharded) path.
+ * ------------------------------------------------------------------------- */
+
+/* Scratch bytes pmm_topk_f32_device needs for this problem. */
+size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int metric,
+                                int compute);
+
+/* Fused top-k over device buffers.  ldq / ldc are row strides in elements;
+ * d must be a multiple of 32 and ldq/ldc multiples of 4 with 16-byte-aligned
+ * bases (pmm_topk_f32 pads host inputs itself).  index_base is added to every
+ * returned corpus index (global index of corpus row 0 of this shard).
+ * workspace may be NULL (allocated stream-ordered and cached per thread). */
+int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, int64_t ldc,
+                        int64_t n, int64_t d, int64_t k, int metric, int compute,
+                        uint32_t index_base, uint32_t *out_idx, float *out_score,
+                        void *workspace, size_t workspace_bytes, void *stream);
+
+/* k-way merge of per-shard top-k lists: idx/score are [m][lists][k_in] (each
+ * list best-first, as pmm_topk_f32_device writes them; idx 0xFFFFFFFF marks
+ * an empty slot).  Writes the best k_out of each row to out_idx/out_score
+ * [m][k_out].  This is the merge step after the RCCL gather of the
+ * corpus-sharded path (no reference counterpart: the reference is
+ * single-process). */
+int pmm_merge_topk_device(const uint32_t *idx, const float *score, int64_t m, int64_t lists,
+                          int64_t k_in, int64_t k_out, int metric, uint32_t *out_idx,
+                          float *out_score, void *stream);
+
+/* Per-kernel timing on the launch stream (hipEvents around each launch).
+ * enable=1 starts recording; pmm_timing_read returns the summed milliseconds
+ * and launch count of kernels whose name contains `kernel` since the last
+ * reset (it synchronises the recorded events). */
+int pmm_timing_enable(int enable);
+int pmm_timing_reset(void);
+int pmm_timing_read(const char *kernel, double *total_ms, int64_t *launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PMM_H_ */

@@ -1,0 +1,741 @@
+// pmm_capi.hip -- C ABI (include/pmm.h) and host orchestration.
+//
+// Host side of the hot path that the reference implements in
+// src/matmul.rs:295-519 (dispatch, extraction, k clipping, error texts) and
+// src/lib.rs:15-55 (the FFI boundary).  Here it owns: per-thread HIP stream
+// and scratch arena, upload/padding of host inputs, the work decomposition of
+// the fused kernel, and the launch sequence norms -> fused GEMM+top-k ->
+// merge.  All device work of one call is enqueued on one stream; host calls
+// synchronise that stream once at the end.
+#include "pmm_internal.h"
+#include "../../include/pmm.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+using namespace pmm;
+
+namespace {
+
+constexpr const char *kVersion = "0.1.4+mi355x.r1";
+constexpr size_t kMaterialiseBudget = size_t(2) << 30;  // bytes of score chunk (f64/large-k/matmul)
+
+thread_local std::string t_err;
+
+int fail(int code, const char *fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  t_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(PMM_ERR_HIP, "HIP error %s at %s:%d (%s)", hipGetErrorString(e_),      \
+                  __FILE__, __LINE__, #expr);                                           \
+  } while (0)
+
+struct DeviceInfo {
+  bool probed = false;
+  bool ok = false;
+  int cus = 256;
+  std::string arch;
+};
+std::mutex g_dev_mu;
+std::vector<DeviceInfo> g_dev;
+
+struct TimingRec {
+  const char *name;
+  hipEvent_t a, b;
+};
+
+struct ThreadCtx {
+  int device = -1;
+  std::vector<hipStream_t> streams;  // per device, created lazily, never destroyed
+  std::vector<void *> arena;         // per device scratch arena
+  std::vector<size_t> arena_bytes;
+  bool timing = false;
+  std::vector<TimingRec> recs;
+};
+thread_local ThreadCtx t_ctx;
+
+int ensure_device(int *dev_out) {
+  if (t_ctx.device < 0) {
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur));
+    t_ctx.device = cur;
+  }
+  const int dev = t_ctx.device;
+  {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if ((int)g_dev.size() <= dev) g_dev.resize(dev + 1);
+    DeviceInfo &di = g_dev[dev];
+    if (!di.probed) {
+      hipDeviceProp_t p;
+      hipError_t e = hipGetDeviceProperties(&p, dev);
+      if (e != hipSuccess)
+        return fail(PMM_ERR_NODEVICE, "no HIP device %d: %s", dev, hipGetErrorString(e));
+      di.probed = true;
+      di.arch = p.gcnArchName;
+      di.cus = p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
+      di.ok = di.arch.rfind("gfx950", 0) == 0;
+    }
+    if (!di.ok)
+      return fail(PMM_ERR_NODEVICE,
+                  "libpmm is built for gfx950 (MI355X); HIP device %d is %s", dev, di.arch.c_str());
+  }
+  HIP_TRY(hipSetDevice(dev));
+  *dev_out = dev;
+  return PMM_OK;
+}
+
+int thread_stream(int dev, hipStream_t *s) {
+  if ((int)t_ctx.streams.size() <= dev) t_ctx.streams.resize(dev + 1, nullptr);
+  if (!t_ctx.streams[dev]) HIP_TRY(hipStreamCreateWithFlags(&t_ctx.streams[dev], hipStreamNonBlocking));
+  *s = t_ctx.streams[dev];
+  return PMM_OK;
+}
+
+// Grow-only per-thread, per-device scratch.  Growing waits for the stream so
+// in-flight work never sees its buffer freed.
+int arena(int dev, hipStream_t s, size_t bytes, void **p) {
+  if ((int)t_ctx.arena.size() <= dev) {
+    t_ctx.arena.resize(dev + 1, nullptr);
+    t_ctx.arena_bytes.resize(dev + 1, 0);
+  }
+  if (t_ctx.arena_bytes[dev] < bytes) {
+    if (t_ctx.arena[dev]) {
+      HIP_TRY(hipStreamSynchronize(s));
+      HIP_TRY(hipFree(t_ctx.arena[dev]));
+      t_ctx.arena[dev] = nullptr;
+      t_ctx.arena_bytes[dev] = 0;
+    }
+    size_t want = bytes + bytes / 8;
+    HIP_TRY(hipMalloc(&t_ctx.arena[dev], want));
+    t_ctx.arena_bytes[dev] = want;
+  }
+  *p = t_ctx.arena[dev];
+  return PMM_OK;
+}
+
+size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
+int next_pow2(int x, int lo = 64) {
+  int p = lo;
+  while (p < x) p <<= 1;
+  return p;
+}
+int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+struct Timed {
+  hipStream_t s;
+  TimingRec rec{};
+  bool on;
+  Timed(const char *name, hipStream_t st) : s(st), on(t_ctx.timing) {
+    if (on) {
+      rec.name = name;
+      (void)hipEventCreate(&rec.a);
+      (void)hipEventCreate(&rec.b);
+      (void)hipEventRecord(rec.a, s);
+    }
+  }
+  ~Timed() {
+    if (on) {
+      (void)hipEventRecord(rec.b, s);
+      t_ctx.recs.push_back(rec);
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Work decomposition of the persistent GEMM: units = QB query blocks x S
+// corpus splits of tps tiles.  Minimise rounds * (tps + overhead) over all tps
+// so the last round of units fills the chip, subject to the candidate-buffer
+// memory budget (M * S * capg * 8 bytes).
+// ---------------------------------------------------------------------------
+struct Plan {
+  int QB = 0, T = 0, tps = 0, S = 0, units = 0, grid = 0, capg = 0, P = 0;
+  size_t off_counter = 0, off_gthr = 0, off_cnt = 0, off_cand = 0, off_qn = 0, off_cn = 0;
+  size_t total = 0;
+};
+
+void plan_units(int64_t m, int64_t n, int cus, double unit_overhead, int64_t max_S, Plan &p) {
+  p.QB = (int)cdiv(m, gemm_f32_bm());
+  p.T = (int)cdiv(n, gemm_f32_bn());
+  double best = 1e300;
+  int best_tps = p.T;
+  for (int tps = 1; tps <= p.T; tps++) {
+    const int64_t S = cdiv(p.T, tps);
+    if (S > max_S) continue;
+    if (tps > 1 && cdiv(p.T, tps - 1) == S) continue;  // same S, fewer tiles: dominated
+    const int64_t units = (int64_t)p.QB * S;
+    const int64_t rounds = cdiv(units, cus);
+    const double cost = (double)rounds * (tps + unit_overhead) + 1e-4 * (double)S;
+    if (cost < best) {
+      best = cost;
+      best_tps = tps;
+    }
+  }
+  p.tps = best_tps;
+  p.S = (int)cdiv(p.T, p.tps);
+  p.units = p.QB * p.S;
+  p.grid = (int)std::min<int64_t>(p.units, cus);
+}
+
+int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p) {
+  p.capg = next_pow2((int)k + 64, 128);
+  const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
+  const size_t cand_budget = size_t(8) << 30;
+  int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
+  plan_units(m, n, cus, 0.5, max_S, p);
+  p.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
+  size_t off = 0;
+  p.off_counter = off;
+  off += 256;
+  p.off_gthr = off;
+  off = al256(off + (size_t)m * 8);
+  p.off_cnt = off;
+  off = al256(off + (size_t)m * p.S * 4);
+  p.off_cand = off;
+  off = al256(off + (size_t)m * p.S * p.capg * 8);
+  p.off_qn = off;
+  off = al256(off + (metric != kMetricDot ? (size_t)m * 4 : 0));
+  p.off_cn = off;
+  off = al256(off + (metric != kMetricDot ? (size_t)n * 4 : 0));
+  p.total = off;
+  (void)d;
+  return PMM_OK;
+}
+
+// Materialised path (k > kFusedMaxK, f32): rows per chunk and workspace.
+struct MatPlan {
+  int64_t rows = 0;
+  int P = 0, P2 = 0;
+  bool global_sort = false;
+  size_t off_counter = 0, off_qn = 0, off_cn = 0, off_scores = 0, off_keys = 0, total = 0;
+};
+
+void plan_materialise(int64_t m, int64_t n, int64_t k, size_t elem, MatPlan &p) {
+  p.P = next_pow2(2 * (int)std::min<int64_t>(k, 1 << 20) + 64, 128);
+  p.global_sort = (k > (kRowSelMaxP - 64) / 2) || p.P > kRowSelMaxP;
+  p.P2 = p.global_sort ? next_pow2((int)n, 2) : 0;
+  size_t per_row = (size_t)n * elem + (p.global_sort ? (size_t)p.P2 * 16 : 0);
+  p.rows = std::max<int64_t>(1, std::min<int64_t>(m, (int64_t)(kMaterialiseBudget / per_row)));
+  size_t off = 0;
+  p.off_counter = off;
+  off += 256;
+  p.off_qn = off;
+  off = al256(off + (size_t)m * elem);
+  p.off_cn = off;
+  off = al256(off + (size_t)n * elem);
+  p.off_scores = off;
+  off = al256(off + (size_t)p.rows * n * elem);
+  p.off_keys = off;
+  off = al256(off + (p.global_sort ? (size_t)p.rows * p.P2 * 16 : 0));
+  p.total = off;
+}
+
+int check_metric(int metric) {
+  if (metric != kMetricCosine && metric != kMetricDot && metric != kMetricEuclidean)
+    return fail(PMM_ERR_ARG, "invalid metric id %d", metric);
+  return PMM_OK;
+}
+
+// Store-mode GEMM over rows [0, rows) of q into out (ldo), raw or transformed.
+int gemm_store_f32(const float *q, int64_t ldq, int64_t rows, const float *c, int64_t ldc, int64_t n,
+                   int64_t d, int metric, int store_metric, const float *qn, const float *cn,
+                   float *out, int64_t ldo, unsigned *counter, int cus, hipStream_t s) {
+  Plan p;
+  plan_units(rows, n, cus, 0.1, 1 << 20, p);
+  GemmF32Args a{};
+  a.q = q;
+  a.c = c;
+  a.qn = qn;
+  a.cn = cn;
+  a.ldq = ldq;
+  a.ldc = ldc;
+  a.M = (int)rows;
+  a.N = (int)n;
+  a.D = (int)d;
+  a.k = 0;
+  a.capg = 0;
+  a.metric = metric;
+  a.QB = p.QB;
+  a.S = p.S;
+  a.tps = p.tps;
+  a.ntiles = p.T;
+  a.units = p.units;
+  a.counter = counter;
+  a.out = out;
+  a.ldo = ldo;
+  a.store_metric = store_metric;
+  HIP_TRY(hipMemsetAsync(counter, 0, 4, s));
+  Timed t(store_metric ? "gemm_f32_scores" : "gemm_f32_matmul", s);
+  HIP_TRY(launch_gemm_f32(a, 1, p.grid, s));
+  return PMM_OK;
+}
+
+int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c, int64_t ldc,
+                         int64_t n, int64_t d, int64_t k, int metric, uint32_t index_base,
+                         uint32_t *out_idx, float *out_score, void *ws, size_t ws_bytes,
+                         hipStream_t s, int dev) {
+  const int cus = g_dev[dev].cus;
+  if (k <= kFusedMaxK) {
+    Plan p;
+    plan_topk(m, n, d, k, metric, cus, p);
+    if (!ws) {
+      int rc = arena(dev, s, p.total, &ws);
+      if (rc) return rc;
+    } else if (ws_bytes < p.total) {
+      return fail(PMM_ERR_ARG, "workspace too small: %zu < %zu bytes", ws_bytes, p.total);
+    }
+    char *w = (char *)ws;
+    float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
+    HIP_TRY(hipMemsetAsync(w, 0, p.off_gthr + (size_t)m * 8, s));
+    if (metric != kMetricDot) {
+      const int sq = metric == kMetricEuclidean;
+      Timed t("norms_f32", s);
+      HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, s));
+      HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, s));
+    }
+    GemmF32Args a{};
+    a.q = q;
+    a.c = c;
+    a.qn = qn;
+    a.cn = cn;
+    a.ldq = ldq;
+    a.ldc = ldc;
+    a.M = (int)m;
+    a.N = (int)n;
+    a.D = (int)d;
+    a.k = (int)k;
+    a.capg = p.capg;
+    a.metric = metric;
+    a.QB = p.QB;
+    a.S = p.S;
+    a.tps = p.tps;
+    a.ntiles = p.T;
+    a.units = p.units;
+    a.counter = (unsigned *)(w + p.off_counter);
+    a.cand = (unsigned long long *)(w + p.off_cand);
+    a.cnt = (unsigned *)(w + p.off_cnt);
+    a.gthr = (unsigned long long *)(w + p.off_gthr);
+    {
+      Timed t("gemm_f32_topk", s);
+      HIP_TRY(launch_gemm_f32(a, 0, p.grid, s));
+    }
+    MergeArgs ma{};
+    ma.cand = a.cand;
+    ma.cnt = a.cnt;
+    ma.gthr = a.gthr;
+    ma.capg = p.capg;
+    ma.M = (int)m;
+    ma.S = p.S;
+    ma.k_out = (int)k;
+    ma.P = p.P;
+    ma.metric = metric;
+    ma.index_base = index_base;
+    ma.out_idx = out_idx;
+    ma.out_score = out_score;
+    {
+      Timed t("merge_topk", s);
+      HIP_TRY(launch_merge(ma, 0, s));
+    }
+    return PMM_OK;
+  }
+  // k beyond the fused path: materialise score chunks, row-select them.
+  MatPlan p;
+  plan_materialise(m, n, k, 4, p);
+  if (!ws) {
+    int rc = arena(dev, s, p.total, &ws);
+    if (rc) return rc;
+  } else if (ws_bytes < p.total) {
+    return fail(PMM_ERR_ARG, "workspace too small: %zu < %zu bytes", ws_bytes, p.total);
+  }
+  char *w = (char *)ws;
+  float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
+  float *sc = (float *)(w + p.off_scores);
+  if (metric != kMetricDot) {
+    const int sq = metric == kMetricEuclidean;
+    HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, s));
+    HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, s));
+  }
+  for (int64_t r0 = 0; r0 < m; r0 += p.rows) {
+    const int64_t rows = std::min<int64_t>(p.rows, m - r0);
+    int rc = gemm_store_f32(q + r0 * ldq, ldq, rows, c, ldc, n, d, metric, 1, qn + r0, cn, sc, n,
+                            (unsigned *)(w + p.off_counter), cus, s);
+    if (rc) return rc;
+    if (!p.global_sort) {
+      RowSelArgs ra{};
+      ra.scores = sc;
+      ra.lds = n;
+      ra.rows = (int)rows;
+      ra.N = (int)n;
+      ra.k = (int)k;
+      ra.P = p.P;
+      ra.metric = metric;
+      ra.is_f64 = 0;
+      ra.index_base = index_base;
+      ra.out_idx = out_idx + r0 * k;
+      ra.out_score = out_score + r0 * k;
+      HIP_TRY(launch_rowselect(ra, s));
+    } else {
+      HIP_TRY(launch_rowsort_global(sc, n, (int)rows, (int)n, 0, metric, w + p.off_keys, p.P2,
+                                    (int)k, index_base, out_idx + r0 * k, out_score + r0 * k, s));
+    }
+  }
+  return PMM_OK;
+}
+
+// Upload a host matrix rows x d into a device buffer with row stride dp,
+// zero-padding columns d..dp-1.
+int upload_padded(void *dst, const void *src, int64_t rows, int64_t d, int64_t dp, size_t elem,
+                  hipStream_t s) {
+  if (rows <= 0) return PMM_OK;
+  if (dp == d) {
+    HIP_TRY(hipMemcpyAsync(dst, src, (size_t)rows * d * elem, hipMemcpyHostToDevice, s));
+  } else {
+    HIP_TRY(hipMemsetAsync(dst, 0, (size_t)rows * dp * elem, s));
+    HIP_TRY(hipMemcpy2DAsync(dst, (size_t)dp * elem, src, (size_t)d * elem, (size_t)d * elem,
+                             (size_t)rows, hipMemcpyHostToDevice, s));
+  }
+  return PMM_OK;
+}
+
+int validate_sizes(int64_t m, int64_t n, int64_t d, int64_t k, bool topk) {
+  if (m < 0 || n < 0 || d < 0) return fail(PMM_ERR_ARG, "negative size (m=%lld n=%lld d=%lld)",
+                                           (long long)m, (long long)n, (long long)d);
+  if (m > INT32_MAX || n > (int64_t)UINT32_MAX - 1 || n > INT32_MAX)
+    return fail(PMM_ERR_ARG, "size out of range (m=%lld n=%lld)", (long long)m, (long long)n);
+  if (topk) {
+    if (k < 0) return fail(PMM_ERR_ARG, "k must be >= 0 (got %lld)", (long long)k);
+    if (k > n) return fail(PMM_ERR_ARG, "k (%lld) must be <= n (%lld): clip k to n first",
+                           (long long)k, (long long)n);
+  }
+  return PMM_OK;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+const char *pmm_version(void) { return kVersion; }
+
+const char *pmm_last_error(void) { return t_err.c_str(); }
+
+int pmm_metric_from_str(const char *s, int *metric) {
+  if (!s || !metric) return fail(PMM_ERR_ARG, "null argument");
+  std::string l(s);
+  for (auto &ch : l) ch = (char)tolower((unsigned char)ch);
+  if (l == "cosine") *metric = PMM_METRIC_COSINE;
+  else if (l == "dot") *metric = PMM_METRIC_DOT;
+  else if (l == "euclidean" || l == "l2") *metric = PMM_METRIC_EUCLIDEAN;
+  else return fail(PMM_ERR_ARG, "Unknown metric: '%s'. Supported: cosine, dot, euclidean", s);
+  return PMM_OK;
+}
+
+int pmm_metric_higher_is_better(int metric) { return metric != PMM_METRIC_EUCLIDEAN; }
+
+int pmm_device_count(int *count) {
+  if (!count) return fail(PMM_ERR_ARG, "null argument");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *count = n;
+  return PMM_OK;
+}
+
+int pmm_set_device(int device) {
+  int n = 0;
+  pmm_device_count(&n);
+  if (device < 0 || device >= n) return fail(PMM_ERR_NODEVICE, "no HIP device %d (%d visible)", device, n);
+  HIP_TRY(hipSetDevice(device));
+  t_ctx.device = device;
+  return PMM_OK;
+}
+
+size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int metric,
+                                int compute) {
+  (void)compute;
+  int cus = 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if ((int)g_dev.size() > dev && g_dev[dev].probed) cus = g_dev[dev].cus;
+  }
+  if (k <= kFusedMaxK) {
+    Plan p;
+    plan_topk(m, n, d, k, metric, cus, p);
+    return p.total;
+  }
+  MatPlan p;
+  plan_materialise(m, n, k, 4, p);
+  return p.total;
+}
+
+int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, int64_t ldc,
+                        int64_t n, int64_t d, int64_t k, int metric, int compute,
+                        uint32_t index_base, uint32_t *out_idx, float *out_score, void *workspace,
+                        size_t workspace_bytes, void *stream) {
+  int rc = validate_sizes(m, n, d, k, true);
+  if (rc) return rc;
+  if ((rc = check_metric(metric))) return rc;
+  if (compute != PMM_COMPUTE_F32)
+    return fail(PMM_ERR_UNSUPPORTED, "compute mode %d not available in this build", compute);
+  if (m == 0 || k == 0) return PMM_OK;
+  if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
+  if (d % 32 != 0 || ldq % 4 != 0 || ldc % 4 != 0 || ldq < d || ldc < d ||
+      ((uintptr_t)q & 15) || ((uintptr_t)c & 15))
+    return fail(PMM_ERR_ARG,
+                "device inputs need d %% 32 == 0, 16-byte-aligned rows (d=%lld ldq=%lld ldc=%lld)",
+                (long long)d, (long long)ldq, (long long)ldc);
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (!s && (rc = thread_stream(dev, &s))) return rc;
+  return topk_f32_device_impl(q, ldq, m, c, ldc, n, d, k, metric, index_base, out_idx, out_score,
+                              workspace, workspace_bytes, s, dev);
+}
+
+int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_t d, int64_t k,
+                    int metric, int compute, uint32_t *out_idx, float *out_score) {
+  int rc = validate_sizes(m, n, d, k, true);
+  if (rc) return rc;
+  if ((rc = check_metric(metric))) return rc;
+  if (compute != PMM_COMPUTE_F32)
+    return fail(PMM_ERR_UNSUPPORTED, "compute mode %d not available in this build", compute);
+  if (m == 0 || k == 0) return PMM_OK;
+  if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
+  if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s;
+  if ((rc = thread_stream(dev, &s))) return rc;
+  const int64_t dp = cdiv(d, 32) * 32;
+  size_t ws_need = pmm_topk_workspace_bytes(m, n, dp, k, metric, compute);
+  size_t off_q = 0, off_c = al256((size_t)m * dp * 4), off_i = off_c + al256((size_t)n * dp * 4);
+  size_t off_s = off_i + al256((size_t)m * k * 4), off_w = off_s + al256((size_t)m * k * 4);
+  void *base;
+  if ((rc = arena(dev, s, off_w + ws_need, &base))) return rc;
+  char *b = (char *)base;
+  if ((rc = upload_padded(b + off_q, q, m, d, dp, 4, s))) return rc;
+  if ((rc = upload_padded(b + off_c, c, n, d, dp, 4, s))) return rc;
+  rc = topk_f32_device_impl((const float *)(b + off_q), dp, m, (const float *)(b + off_c), dp, n,
+                            dp, k, metric, 0u, (uint32_t *)(b + off_i), (float *)(b + off_s),
+                            b + off_w, ws_need, s, dev);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return PMM_OK;
+}
+
+int pmm_topk_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d, int64_t k,
+                 int metric, uint32_t *out_idx, float *out_score) {
+  return pmm_topk_f32_ex(q, m, c, n, d, k, metric, PMM_COMPUTE_F32, out_idx, out_score);
+}
+
+int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t d, int64_t k,
+                 int metric, uint32_t *out_idx, double *out_score) {
+  int rc = validate_sizes(m, n, d, k, true);
+  if (rc) return rc;
+  if ((rc = check_metric(metric))) return rc;
+  if (m == 0 || k == 0) return PMM_OK;
+  if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
+  if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s;
+  if ((rc = thread_stream(dev, &s))) return rc;
+  const int64_t dp = cdiv(d, 16) * 16;
+  MatPlan p;
+  plan_materialise(m, n, k, 8, p);
+  size_t off_q = 0, off_c = al256((size_t)m * dp * 8), off_i = off_c + al256((size_t)n * dp * 8);
+  size_t off_s = off_i + al256((size_t)m * k * 4), off_w = off_s + al256((size_t)m * k * 8);
+  void *base;
+  if ((rc = arena(dev, s, off_w + p.total, &base))) return rc;
+  char *b = (char *)base;
+  char *w = b + off_w;
+  const double *dq = (const double *)(b + off_q), *dc = (const double *)(b + off_c);
+  if ((rc = upload_padded(b + off_q, q, m, d, dp, 8, s))) return rc;
+  if ((rc = upload_padded(b + off_c, c, n, d, dp, 8, s))) return rc;
+  double *qn = (double *)(w + p.off_qn), *cn = (double *)(w + p.off_cn);
+  double *sc = (double *)(w + p.off_scores);
+  if (metric != kMetricDot) {
+    const int sq = metric == kMetricEuclidean;
+    HIP_TRY(launch_norms_f64(dq, m, d, dp, sq, qn, s));
+    HIP_TRY(launch_norms_f64(dc, n, d, dp, sq, cn, s));
+  }
+  uint32_t *oi = (uint32_t *)(b + off_i);
+  double *os = (double *)(b + off_s);
+  for (int64_t r0 = 0; r0 < m; r0 += p.rows) {
+    const int64_t rows = std::min<int64_t>(p.rows, m - r0);
+    {
+      Timed t("gemm_f64_scores", s);
+      HIP_TRY(launch_gemm_f64_store(dq + r0 * dp, dp, dc, dp, qn + r0, cn, (int)rows, (int)n,
+                                    (int)dp, metric, 1, sc, n, s));
+    }
+    if (!p.global_sort) {
+      RowSelArgs ra{};
+      ra.scores = sc;
+      ra.lds = n;
+      ra.rows = (int)rows;
+      ra.N = (int)n;
+      ra.k = (int)k;
+      ra.P = p.P;
+      ra.metric = metric;
+      ra.is_f64 = 1;
+      ra.index_base = 0;
+      ra.out_idx = oi + r0 * k;
+      ra.out_score = os + r0 * k;
+      HIP_TRY(launch_rowselect(ra, s));
+    } else {
+      HIP_TRY(launch_rowsort_global(sc, n, (int)rows, (int)n, 1, metric, w + p.off_keys, p.P2,
+                                    (int)k, 0u, oi + r0 * k, os + r0 * k, s));
+    }
+  }
+  HIP_TRY(hipMemcpyAsync(out_idx, oi, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(out_score, os, (size_t)m * k * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return PMM_OK;
+}
+
+int pmm_matmul_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d, float *out) {
+  int rc = validate_sizes(m, n, d, 0, false);
+  if (rc) return rc;
+  if (m == 0 || n == 0) return PMM_OK;
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s;
+  if ((rc = thread_stream(dev, &s))) return rc;
+  const int64_t dp = cdiv(std::max<int64_t>(d, 1), 32) * 32;
+  const int64_t rows_chunk =
+      std::max<int64_t>(1, std::min<int64_t>(m, (int64_t)(kMaterialiseBudget / ((size_t)n * 4))));
+  size_t off_q = 0, off_c = al256((size_t)m * dp * 4), off_o = off_c + al256((size_t)n * dp * 4);
+  size_t off_cnt = off_o + al256((size_t)rows_chunk * n * 4);
+  void *base;
+  if ((rc = arena(dev, s, off_cnt + 256, &base))) return rc;
+  char *b = (char *)base;
+  if ((rc = upload_padded(b + off_q, q, m, d, dp, 4, s))) return rc;
+  if ((rc = upload_padded(b + off_c, c, n, d, dp, 4, s))) return rc;
+  const float *dq = (const float *)(b + off_q), *dc = (const float *)(b + off_c);
+  float *dout = (float *)(b + off_o);
+  for (int64_t r0 = 0; r0 < m; r0 += rows_chunk) {
+    const int64_t rows = std::min<int64_t>(rows_chunk, m - r0);
+    rc = gemm_store_f32(dq + r0 * dp, dp, rows, dc, dp, n, dp, kMetricDot, 0, nullptr, nullptr,
+                        dout, n, (unsigned *)(b + off_cnt), g_dev[dev].cus, s);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out + r0 * n, dout, (size_t)rows * n * 4, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return PMM_OK;
+}
+
+int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t d,
+                   double *out) {
+  int rc = validate_sizes(m, n, d, 0, false);
+  if (rc) return rc;
+  if (m == 0 || n == 0) return PMM_OK;
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s;
+  if ((rc = thread_stream(dev, &s))) return rc;
+  const int64_t dp = cdiv(std::max<int64_t>(d, 1), 16) * 16;
+  const int64_t rows_chunk =
+      std::max<int64_t>(1, std::min<int64_t>(m, (int64_t)(kMaterialiseBudget / ((size_t)n * 8))));
+  size_t off_q = 0, off_c = al256((size_t)m * dp * 8), off_o = off_c + al256((size_t)n * dp * 8);
+  void *base;
+  if ((rc = arena(dev, s, off_o + al256((size_t)rows_chunk * n * 8), &base))) return rc;
+  char *b = (char *)base;
+  if ((rc = upload_padded(b + off_q, q, m, d, dp, 8, s))) return rc;
+  if ((rc = upload_padded(b + off_c, c, n, d, dp, 8, s))) return rc;
+  const double *dq = (const double *)(b + off_q), *dc = (const double *)(b + off_c);
+  double *dout = (double *)(b + off_o);
+  for (int64_t r0 = 0; r0 < m; r0 += rows_chunk) {
+    const int64_t rows = std::min<int64_t>(rows_chunk, m - r0);
+    {
+      Timed t("gemm_f64_matmul", s);
+      HIP_TRY(launch_gemm_f64_store(dq + r0 * dp, dp, dc, dp, nullptr, nullptr, (int)rows, (int)n,
+                                    (int)dp, kMetricDot, 0, dout, n, s));
+    }
+    HIP_TRY(hipMemcpyAsync(out + r0 * n, dout, (size_t)rows * n * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return PMM_OK;
+}
+
+int pmm_merge_topk_device(const uint32_t *idx, const float *score, int64_t m, int64_t lists,
+                          int64_t k_in, int64_t k_out, int metric, uint32_t *out_idx,
+                          float *out_score, void *stream) {
+  int rc;
+  if ((rc = check_metric(metric))) return rc;
+  if (m < 0 || lists < 1 || k_in < 0 || k_out < 0 || k_out > lists * k_in)
+    return fail(PMM_ERR_ARG, "bad merge sizes (m=%lld lists=%lld k_in=%lld k_out=%lld)",
+                (long long)m, (long long)lists, (long long)k_in, (long long)k_out);
+  if (k_out > kFusedMaxK) return fail(PMM_ERR_UNSUPPORTED, "merge k_out > %d", kFusedMaxK);
+  if (m == 0 || k_out == 0) return PMM_OK;
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  if (!s && (rc = thread_stream(dev, &s))) return rc;
+  MergeArgs ma{};
+  ma.in_idx = idx;
+  ma.in_score = score;
+  ma.k_in = (int)k_in;
+  ma.M = (int)m;
+  ma.S = (int)lists;
+  ma.k_out = (int)k_out;
+  ma.P = std::min(8192, next_pow2(2 * (int)k_out + 64, 128));
+  ma.metric = metric;
+  ma.out_idx = out_idx;
+  ma.out_score = out_score;
+  Timed t("merge_shards", s);
+  HIP_TRY(launch_merge(ma, 1, s));
+  return PMM_OK;
+}
+
+int pmm_timing_enable(int enable) {
+  t_ctx.timing = enable != 0;
+  return PMM_OK;
+}
+
+int pmm_timing_reset(void) {
+  for (auto &r : t_ctx.recs) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  t_ctx.recs.clear();
+  return PMM_OK;
+}
+
+int pmm_timing_read(const char *kernel, double *total_ms, int64_t *launches) {
+  double tot = 0.0;
+  int64_t cnt = 0;
+  for (auto &r : t_ctx.recs) {
+    if (kernel && !strstr(r.name, kernel)) continue;
+    HIP_TRY(hipEventSynchronize(r.b));
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+    tot += ms;
+    cnt++;
+  }
+  if (total_ms) *total_ms = tot;
+  if (launches) *launches = cnt;
+  return PMM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// pmm_internal.h -- launch-side interface between the host orchestration
+// (pmm_capi.hip) and the gfx950 kernels (pmm_kernels.hip).  Not installed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace pmm {
+
+constexpr int kMetricCosine = 0;
+constexpr int kMetricDot = 1;
+constexpr int kMetricEuclidean = 2;
+
+// Fused top-k path limits.  k above kFusedMaxK goes through the materialise +
+// row-select path (kernels below), which also serves f64.
+constexpr int kFusedMaxK = 1024;
+// Row-select (materialised scores) keeps up to kRowSelMaxP entries per row in
+// LDS; larger k uses the full-row global sort.
+constexpr int kRowSelMaxP = 4096;
+
+// Arguments of the f32 MFMA GEMM kernel (top-k and store modes).
+struct GemmF32Args {
+  const float *q;       // M x ldq
+  const float *c;       // N x ldc
+  const float *qn;      // cosine: L2 norms of Q rows; euclidean: squared norms
+  const float *cn;      // same for C rows
+  int64_t ldq, ldc;
+  int M, N, D;          // D % 32 == 0
+  int k, capg;          // top-k and candidate-buffer capacity (power of two)
+  int metric;
+  int QB, S, tps, ntiles, units;  // work decomposition (see plan_units)
+  unsigned *counter;              // work-queue head, zeroed per call
+  unsigned long long *cand;       // [M*S][capg] candidate composites
+  unsigned *cnt;                  // [M*S] candidate counts
+  unsigned long long *gthr;       // [M] shared per-row threshold, zeroed per call
+  float *out;                     // store mode: out[M][ldo]
+  int64_t ldo;
+  int store_metric;               // store mode: 1 = metric-transformed score, 0 = raw dot
+};
+
+struct MergeArgs {
+  // loader 0: candidate segments from the fused kernel
+  const unsigned long long *cand;
+  const unsigned *cnt;
+  const unsigned long long *gthr;
+  int capg;
+  // loader 1: gathered (idx, score) lists [M][S][k_in]
+  const uint32_t *in_idx;
+  const float *in_score;
+  int k_in;
+  int M, S, k_out, P, metric;
+  uint32_t index_base;
+  uint32_t *out_idx;
+  float *out_score;
+};
+
+struct RowSelArgs {
+  const void *scores;   // [rows][lds] f32 or f64, already metric-transformed
+  int64_t lds;
+  int rows, N, k, P, metric, is_f64;
+  uint32_t index_base;  // added to every output index
+  uint32_t *out_idx;    // [rows][k]
+  void *out_score;      // [rows][k] f32 or f64
+};
+
+// ---- launchers (pmm_kernels.hip) ----
+hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld, int squared,
+                            float *out, hipStream_t s);
+hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,
+                            double *out, hipStream_t s);
+// mode 0 = fused top-k, 1 = store.  grid = number of persistent workgroups.
+hipError_t launch_gemm_f32(const GemmF32Args &a, int mode, int grid, hipStream_t s);
+int gemm_f32_bm();   // rows per workgroup
+int gemm_f32_bn();   // corpus columns per tile
+size_t gemm_f32_lds_bytes(int mode, int capg);
+hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s);
+size_t merge_lds_bytes_per_wave(int P);
+hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, int64_t ldc,
+                                 const double *qn, const double *cn, int M, int N, int D,
+                                 int metric, int store_metric, double *out, int64_t ldo,
+                                 hipStream_t s);
+hipError_t launch_rowselect(const RowSelArgs &a, hipStream_t s);
+// full-row sort fallback for very large k
+hipError_t launch_rowsort_global(const void *scores, int64_t lds, int rows, int N, int is_f64,
+                                 int metric, void *keys_ws, int P2, int k, uint32_t index_base,
+                                 uint32_t *out_idx,
+                                 void *out_score, hipStream_t s);
+
+}  // namespace pmm

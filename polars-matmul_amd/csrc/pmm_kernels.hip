@@ -1,0 +1,884 @@
+// pmm_kernels.hip -- gfx950 (MI355X / CDNA4) kernels of the similarity-search
+// engine behind `.pmm.topk` / `.pmm.matmul`.
+//
+// Replaces, in one device pipeline, the reference's CPU chain
+//   compute_norms_f32 (src/metrics.rs:382-393) ->
+//   matmul_f32 via faer (src/metrics.rs:204-255) ->
+//   cosine / euclidean epilogue over the full M x N matrix (src/metrics.rs:314-365) ->
+//   select_topk_with_scores_f32 (src/topk.rs:42-75)
+// with: an ndarray-order norm kernel, an f32 MFMA GEMM whose epilogue applies
+// the metric and runs a threshold-pruned per-row top-k (the M x N score matrix
+// never reaches HBM), and a merge kernel.  The same GEMM main loop in "store"
+// mode is `.pmm.matmul` (src/metrics.rs:160-202).  f64 inputs use an f64 MFMA
+// GEMM plus a row-select kernel (src/metrics.rs:258-311, src/topk.rs:6-39).
+//
+// Built with -ffp-contract=off: every FMA here is an explicit fmaf()/MFMA, so
+// the epilogue arithmetic follows the reference's operation order.
+#include "pmm_internal.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace pmm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned long long u64;
+
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+// ===========================================================================
+// Ordered keys.  The selection order is a total order on (score, index):
+// best score first, NaN last, equal scores -> lower corpus index first.  A
+// score maps to an unsigned key that is monotone in the ranking value
+// (score for cosine/dot, -distance for euclidean); -0 folds onto +0 and NaN
+// maps to 0.  A candidate is the 64-bit composite (key << 32) | ~index, so a
+// single unsigned compare implements the whole order and every composite in
+// a row is unique.
+// ===========================================================================
+__device__ __forceinline__ uint32_t okey32(float v) {
+  if (v != v) return 0u;
+  uint32_t u = __float_as_uint(v);
+  if ((u << 1) == 0u) u = 0u;
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float dekey32(uint32_t k) {
+  if (k == 0u) return __uint_as_float(0x7FC00000u);
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+__device__ __forceinline__ u64 okey64(double v) {
+  if (v != v) return 0ull;
+  u64 u = (u64)__double_as_longlong(v);
+  if ((u << 1) == 0ull) u = 0ull;
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dekey64(u64 k) {
+  if (k == 0ull) return __longlong_as_double(0x7FF8000000000000ll);
+  return __longlong_as_double((long long)((k & 0x8000000000000000ull) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k));
+}
+
+// ===========================================================================
+// Wave primitives (wave64).
+// ===========================================================================
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ int lanes_below(u64 mask) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Bitonic sort, best (largest) first, of P (power of two) u64 in LDS by one wave.
+__device__ void wave_sort_desc_u64(u64 *s, int P, int lane) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < (P >> 1); i += 64) {
+        const int x0 = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
+        const int x1 = x0 + stride;
+        const u64 a = s[x0], b = s[x1];
+        const bool desc = (x0 & size) == 0;
+        if (desc ? (a < b) : (a > b)) {
+          s[x0] = b;
+          s[x1] = a;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
+// 16-byte entry for the materialised (row-select) path: f64 keys need all
+// 64 bits, so the index rides alongside.
+struct __attribute__((aligned(16))) Ent {
+  u64 key;
+  uint32_t idx;
+  uint32_t pad;
+};
+__device__ __forceinline__ bool ent_better(const Ent &a, const Ent &b) {
+  return a.key > b.key || (a.key == b.key && a.idx < b.idx);
+}
+__device__ void wave_sort_desc_ent(Ent *s, int P, int lane) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < (P >> 1); i += 64) {
+        const int x0 = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
+        const int x1 = x0 + stride;
+        const Ent a = s[x0], b = s[x1];
+        const bool desc = (x0 & size) == 0;
+        if (desc ? ent_better(b, a) : ent_better(a, b)) {
+          s[x0] = b;
+          s[x1] = a;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
+__device__ __forceinline__ int next_pow2_dev(int x) {
+  int p = 64;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// ===========================================================================
+// Row norms in ndarray's `unrolled_dot` order (src/metrics.rs:368-393 ->
+// ndarray 0.16 unrolled_dot): accumulator j sums x[8t+j]^2 sequentially,
+// combined as ((((0+(p0+p4))+(p1+p5))+(p2+p6))+(p3+p7)) then the scalar tail.
+// 8 lanes per row, lane j owns accumulator p_j -> bit-identical to the
+// reference's norms (no FMA: the file is built with -ffp-contract=off).
+// ===========================================================================
+template <typename T>
+__device__ __forceinline__ T sqrt_rn(T x);
+template <>
+__device__ __forceinline__ float sqrt_rn<float>(float x) { return __fsqrt_rn(x); }
+template <>
+__device__ __forceinline__ double sqrt_rn<double>(double x) { return __dsqrt_rn(x); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void norms_kernel(const T *__restrict__ a, int64_t rows,
+                                                    int64_t d, int64_t ld, int squared,
+                                                    T *__restrict__ out) {
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = gt >> 3;
+  const int j = threadIdx.x & 7;
+  const bool valid = row < rows;
+  const T *p = a + (valid ? row : 0) * ld;
+  const int64_t d8 = d & ~(int64_t)7;
+  T acc = (T)0;
+  if (valid) {
+    for (int64_t i = j; i < d8; i += 8) {
+      const T x = p[i];
+      acc = acc + x * x;
+    }
+  }
+  const int base = (int)(threadIdx.x & 63) & ~7;
+  T pp[8];
+#pragma unroll
+  for (int t = 0; t < 8; t++) pp[t] = __shfl(acc, base + t, 64);
+  if (valid && j == 0) {
+    T sum = (T)0;
+    sum = sum + (pp[0] + pp[4]);
+    sum = sum + (pp[1] + pp[5]);
+    sum = sum + (pp[2] + pp[6]);
+    sum = sum + (pp[3] + pp[7]);
+    for (int64_t i = d8; i < d; i++) {
+      const T x = p[i];
+      sum = sum + x * x;
+    }
+    out[row] = squared ? sum : sqrt_rn<T>(sum);
+  }
+}
+
+hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld, int squared,
+                            float *out, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  const int64_t threads = rows * 8;
+  const unsigned grid = (unsigned)((threads + 255) / 256);
+  norms_kernel<float><<<grid, 256, 0, s>>>(a, rows, d, ld, squared, out);
+  return hipGetLastError();
+}
+hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,
+                            double *out, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  const int64_t threads = rows * 8;
+  const unsigned grid = (unsigned)((threads + 255) / 256);
+  norms_kernel<double><<<grid, 256, 0, s>>>(a, rows, d, ld, squared, out);
+  return hipGetLastError();
+}
+
+// ===========================================================================
+// Epilogue arithmetic, exactly as the reference orders it.
+//   cosine   (metrics.rs:329-343): q>1e-6 && c>1e-6 ? dot / (q*c) : 0
+//   euclid   (metrics.rs:347-362): sqrt(max((qsq + csq) - 2*dot, 0)),
+//            Rust f32::max returns the non-NaN operand -> NaN becomes 0.
+// ===========================================================================
+template <int METRIC>
+__device__ __forceinline__ float exact_score(float dot, float qv, float cv) {
+  if (METRIC == kMetricDot) return dot;
+  if (METRIC == kMetricCosine) {
+    if (qv > 1e-6f && cv > 1e-6f) return __fdiv_rn(dot, __fmul_rn(qv, cv));
+    return 0.0f;
+  }
+  const float sq = __fsub_rn(__fadd_rn(qv, cv), 2.0f * dot);
+  const float mx = (sq > 0.0f) ? sq : 0.0f;
+  return __fsqrt_rn(mx);
+}
+template <int METRIC>
+__device__ __forceinline__ double exact_score_f64(double dot, double qv, double cv) {
+  if (METRIC == kMetricDot) return dot;
+  if (METRIC == kMetricCosine) {
+    if (qv > 1e-10 && cv > 1e-10) return __ddiv_rn(dot, __dmul_rn(qv, cv));
+    return 0.0;
+  }
+  const double sq = __dsub_rn(__dadd_rn(qv, cv), 2.0 * dot);
+  const double mx = (sq > 0.0) ? sq : 0.0;
+  return __dsqrt_rn(mx);
+}
+
+// Pre-filter bound.  The pre-filter value pv of a score is
+//   dot:    pv = dot                       (exact)
+//   cosine: pv = (dot * (1/qn)) * (1/cn)   (<= 6 ulp from the exact score)
+//   euclid: pv = 2*dot - (qsq + csq)       (= -sq exactly)
+// and an element can only beat the row's current k-th composite `thr` if
+// !(pv < lo).  lo is loose by a margin that covers the approximation, so
+// the pre-filter never rejects a true candidate; survivors are re-tested
+// exactly against the composite.
+template <int METRIC>
+__device__ __forceinline__ float prefilter_lo(u64 thr) {
+  if (thr == ~0ull) return __builtin_inff();             // padding row: reject all
+  const uint32_t tk = (uint32_t)(thr >> 32);
+  if (tk == 0u) return -__builtin_inff();                 // row not full: accept all
+  const float v = dekey32(tk);                            // ranking value of the k-th
+  if (METRIC == kMetricDot) return v;
+  if (METRIC == kMetricCosine) return v - (fabsf(v) * 0x1p-20f + 0x1p-100f);
+  const float dist = -v;
+  const float hi = dist * dist * (1.0f + 0x1p-20f) + 0x1p-100f;
+  return -hi;
+}
+
+// ===========================================================================
+// f32 MFMA GEMM: S = Q * C^T on v_mfma_f32_32x32x2_f32 (exact f32 FMA chain).
+//
+// Work unit = (query block of BM rows) x (corpus split of tps tiles of BN
+// columns); persistent workgroups pull units from a counter, split-major, so
+// the workgroups running together stream the same corpus tiles through the
+// XCD L2s.  Workgroup = NW waves; wave w owns query rows [32w, 32w+32) of the
+// block and all BN columns (NB 32x32 accumulators), so every per-row top-k
+// state has exactly one owning wave and needs no cross-wave sync.
+//
+// K loop (BK = 32 floats): the corpus tile is staged HBM -> LDS with
+// global_load_lds_dwordx4 (double-buffered, XOR-swizzled on the source
+// address so the ds_read_b128 fragment reads are conflict-free); each wave's
+// query fragment goes straight to VGPRs (not shared between waves).  Lane
+// (r = lane&31, h = lane>>5) covers k = 16h..16h+15 of the step, so MFMA
+// substep s pairs k = s and k = 16+s (the dot product is order-free; f32
+// rounding differs from faer's order only within the stated tolerance).
+// ===========================================================================
+constexpr int NB = 4;             // 32-column MFMA blocks per wave
+constexpr int NW = 4;             // waves per workgroup
+constexpr int BN = 32 * NB;       // corpus columns per tile
+constexpr int BM = 32 * NW;       // query rows per workgroup
+constexpr int BT = BN * 128;      // bytes per staged corpus tile (BN x 32 f32)
+constexpr int GLDS_PER_WAVE = BT / 1024 / NW;
+static_assert(BT % (1024 * NW) == 0, "corpus tile must split into 1 KiB LDS-DMA pieces per wave");
+
+int gemm_f32_bm() { return BM; }
+int gemm_f32_bn() { return BN; }
+
+// LDS: [B stage 0 | B stage 1 | thr[BM] u64 | cnt[BM] u32 | unit | scratch NW*capg u64]
+constexpr int LDS_OFF_THR = 2 * BT;
+constexpr int LDS_OFF_CNT = LDS_OFF_THR + BM * 8;
+constexpr int LDS_OFF_UNIT = LDS_OFF_CNT + BM * 4;
+constexpr int LDS_OFF_SCR = LDS_OFF_UNIT + 16;
+static_assert(LDS_OFF_SCR % 16 == 0, "LDS carve must stay 16-byte aligned");
+
+size_t gemm_f32_lds_bytes(int mode, int capg) {
+  return (size_t)LDS_OFF_SCR + (mode == 0 ? (size_t)NW * capg * 8 : 0);
+}
+
+__device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
+
+__device__ __forceinline__ void stage_b(const float *__restrict__ c, int64_t ldc, int col0, int N,
+                                        int kofs, char *buf, int wid, int lane) {
+#pragma unroll
+  for (int i = 0; i < GLDS_PER_WAVE; i++) {
+    const int blk = i * NW + wid;           // 1 KiB piece = 8 corpus rows x 128 B
+    const int col = blk * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((col >> 1) & 7);
+    const int gcol = min(col0 + col, N - 1);
+    const float *src = c + (int64_t)gcol * ldc + kofs + ch * 4;
+    __builtin_amdgcn_global_load_lds((const GLB_AS void *)src, (LDS_AS void *)(buf + blk * 1024),
+                                     16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void load_a(const float *aptr, int kofs, f32x4 (&a)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) a[j] = *(const f32x4 *)(aptr + kofs + 4 * j);
+}
+
+// Wave-level compaction of one row's candidate buffer: sort, keep the best k,
+// raise the row threshold to the k-th composite and publish it (atomicMax)
+// so later units of the same row prune with it.
+__device__ void compact_row(const GemmF32Args &a, int s, int grow, u64 *thr_slot,
+                            unsigned *cnt_slot, u64 *scr, int lane) {
+  u64 *base = a.cand + ((int64_t)grow * a.S + s) * a.capg;
+  const int n = (int)*cnt_slot;
+  const int P = a.capg;
+  for (int i = lane; i < P; i += 64)
+    scr[i] = (i < n) ? __hip_atomic_load(base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : 0ull;
+  wave_sync();
+  wave_sort_desc_u64(scr, P, lane);
+  const int kk = min(a.k, n);
+  for (int i = lane; i < kk; i += 64) base[i] = scr[i];
+  const u64 nt = (n >= a.k) ? scr[a.k - 1] : 0ull;
+  wave_sync();
+  if (lane == 0) {
+    *cnt_slot = (unsigned)kk;
+    if (nt > *thr_slot) *thr_slot = nt;
+    if (nt) atomicMax(a.gthr + grow, nt);
+  }
+  wave_sync();
+}
+
+template <int MODE, int METRIC>
+__global__ __launch_bounds__(NW * 64, 1) void gemm_f32_kernel(GemmF32Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char *bbuf = smem;
+  u64 *thr_l = (u64 *)(smem + LDS_OFF_THR);
+  unsigned *cnt_l = (unsigned *)(smem + LDS_OFF_CNT);
+  int *unit_l = (int *)(smem + LDS_OFF_UNIT);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int KS = a.D >> 5;
+  u64 *scr = (u64 *)(smem + LDS_OFF_SCR) + (size_t)wid * a.capg;
+  u64 *thr_w = thr_l + wid * 32;
+  unsigned *cnt_w = cnt_l + wid * 32;
+  constexpr bool XFORM = (METRIC != kMetricDot);
+
+  for (;;) {
+    if (tid == 0) *unit_l = (int)atomicAdd(a.counter, 1u);
+    __syncthreads();
+    const int unit = *unit_l;
+    __syncthreads();
+    if (unit >= a.units) break;
+    const int s = unit / a.QB;
+    const int qb = unit - s * a.QB;
+    const int t0 = s * a.tps;
+    const int t1 = min(t0 + a.tps, a.ntiles);
+    const int wrow0 = qb * BM + wid * 32;
+    const int arow = min(wrow0 + r32, a.M - 1);
+    const float *aptr = a.q + (int64_t)arow * a.ldq + 16 * h;
+
+    // Per-lane row constants for the 16 accumulator rows this lane holds.
+    float rv[16], lo[16];
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      const int grow = wrow0 + acc_row(e, h);
+      float v = 0.0f;
+      if (XFORM && grow < a.M) {
+        const float x = a.qn[grow];
+        if (MODE == 0 && METRIC == kMetricCosine) v = (x > 1e-6f) ? 1.0f / x : 0.0f;
+        else v = x;
+      }
+      rv[e] = v;
+      lo[e] = 0.0f;
+    }
+    if (MODE == 0) {
+      if (lane < 32) {
+        const int grow = wrow0 + lane;
+        thr_w[lane] = (grow < a.M)
+                          ? __hip_atomic_load(a.gthr + grow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : ~0ull;
+        cnt_w[lane] = 0u;
+      }
+      wave_sync();
+#pragma unroll
+      for (int e = 0; e < 16; e++) lo[e] = prefilter_lo<METRIC>(thr_w[acc_row(e, h)]);
+    }
+
+    const int nsteps = (t1 - t0) * KS;
+    f32x4 acur[4], anext[4];
+    stage_b(a.c, a.ldc, t0 * BN, a.N, 0, bbuf, wid, lane);
+    load_a(aptr, 0, acur);
+    __syncthreads();
+
+    f32x16 acc[NB];
+#pragma unroll
+    for (int c = 0; c < NB; c++) acc[c] = (f32x16){};
+
+    int tile = t0, ks = 0;
+    for (int g = 0; g < nsteps; g++) {
+      int ntile = tile, nks = ks + 1;
+      if (nks == KS) {
+        nks = 0;
+        ntile++;
+      }
+      const bool more = (g + 1) < nsteps;
+      if (more) {
+        stage_b(a.c, a.ldc, ntile * BN, a.N, nks * 32, bbuf + ((g + 1) & 1) * BT, wid, lane);
+        load_a(aptr, nks * 32, anext);
+      }
+      const char *B = bbuf + (g & 1) * BT;
+      const int swz = (r32 >> 1) & 7;
+#pragma unroll
+      for (int qd = 0; qd < 4; qd++) {
+        f32x4 b[NB];
+#pragma unroll
+        for (int c = 0; c < NB; c++) {
+          const int col = 32 * c + r32;
+          b[c] = *(const f32x4 *)(B + col * 128 + 16 * ((4 * h + qd) ^ swz));
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+#pragma unroll
+          for (int c = 0; c < NB; c++)
+            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[qd][j], b[c][j], acc[c], 0, 0, 0);
+        }
+      }
+
+      if (ks == KS - 1) {
+        const int col0 = tile * BN;
+        if (MODE == 1) {
+          // ---- store epilogue (.pmm.matmul, or materialised scores) ----
+#pragma unroll
+          for (int c = 0; c < NB; c++) {
+            const int gcol = col0 + 32 * c + r32;
+            if (gcol < a.N) {
+              const float cv = XFORM ? a.cn[gcol] : 0.0f;
+#pragma unroll
+              for (int e = 0; e < 16; e++) {
+                const int grow = wrow0 + acc_row(e, h);
+                if (grow < a.M) {
+                  const float v = acc[c][e];
+                  a.out[(int64_t)grow * a.ldo + gcol] =
+                      (XFORM && a.store_metric) ? exact_score<METRIC>(v, rv[e], cv) : v;
+                }
+              }
+            }
+          }
+        } else {
+          // ---- fused top-k epilogue ----
+#pragma unroll
+          for (int c = 0; c < NB; c++) {
+            const int gcol = col0 + 32 * c + r32;
+            const bool cvalid = gcol < a.N;
+            const int gcc = min(gcol, a.N - 1);
+            float cv = 0.0f;
+            if (METRIC == kMetricCosine) {
+              const float x = a.cn[gcc];
+              cv = (x > 1e-6f) ? 1.0f / x : 0.0f;
+            } else if (METRIC == kMetricEuclidean) {
+              cv = a.cn[gcc];
+            }
+            bool any = false;
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+              const float v = acc[c][e];
+              float pv;
+              if (METRIC == kMetricDot) pv = v;
+              else if (METRIC == kMetricCosine) pv = (v * rv[e]) * cv;
+              else pv = fmaf(2.0f, v, -(rv[e] + cv));
+              any |= !(pv < lo[e]);
+            }
+            any = any && cvalid;
+            if (__ballot(any) != 0ull) {
+              // exact path: rare after the first tiles of a unit
+              const float cex = XFORM ? a.cn[gcc] : 0.0f;
+#pragma unroll
+              for (int e = 0; e < 16; e++) {
+                const int rl = acc_row(e, h);
+                const int grow = wrow0 + rl;
+                const float qex = XFORM ? a.qn[min(grow, a.M - 1)] : 0.0f;
+                const float sc = exact_score<METRIC>(acc[c][e], qex, cex);
+                const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
+                const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
+                if (cvalid && comp > thr_w[rl]) {
+                  const unsigned pos = atomicAdd(&cnt_w[rl], 1u);
+                  a.cand[((int64_t)grow * a.S + s) * a.capg + pos] = comp;
+                }
+              }
+              wave_sync();
+              const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
+              u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 32));
+              if (need) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                while (need) {
+                  const int r = __builtin_ctzll(need);
+                  need &= need - 1;
+                  compact_row(a, s, wrow0 + r, thr_w + r, cnt_w + r, scr, lane);
+                }
+#pragma unroll
+                for (int e = 0; e < 16; e++) lo[e] = prefilter_lo<METRIC>(thr_w[acc_row(e, h)]);
+              }
+            }
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < NB; c++) acc[c] = (f32x16){};
+      }
+
+      __syncthreads();
+      if (more) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) acur[j] = anext[j];
+      }
+      tile = ntile;
+      ks = nks;
+    }
+
+    if (MODE == 0) {
+      if (lane < 32) {
+        const int grow = wrow0 + lane;
+        if (grow < a.M) a.cnt[(int64_t)grow * a.S + s] = cnt_w[lane];
+      }
+    }
+  }
+}
+
+template <int MODE, int METRIC>
+static hipError_t launch_gemm_f32_t(const GemmF32Args &a, int grid, size_t lds, hipStream_t s) {
+  static bool attr_set = false;  // opt in to > 64 KiB dynamic LDS (large k)
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void *)gemm_f32_kernel<MODE, METRIC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  gemm_f32_kernel<MODE, METRIC><<<dim3(grid), dim3(NW * 64), lds, s>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_f32(const GemmF32Args &a, int mode, int grid, hipStream_t s) {
+  const size_t lds = gemm_f32_lds_bytes(mode, a.capg);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (mode == 0) {
+    if (a.metric == kMetricCosine) return launch_gemm_f32_t<0, kMetricCosine>(a, grid, lds, s);
+    if (a.metric == kMetricDot) return launch_gemm_f32_t<0, kMetricDot>(a, grid, lds, s);
+    return launch_gemm_f32_t<0, kMetricEuclidean>(a, grid, lds, s);
+  }
+  if (!a.store_metric || a.metric == kMetricDot) return launch_gemm_f32_t<1, kMetricDot>(a, grid, lds, s);
+  if (a.metric == kMetricCosine) return launch_gemm_f32_t<1, kMetricCosine>(a, grid, lds, s);
+  return launch_gemm_f32_t<1, kMetricEuclidean>(a, grid, lds, s);
+}
+
+// ===========================================================================
+// Merge: one wave per query row streams candidate entries, keeps those at or
+// above the row threshold in an LDS scratch of P slots, compacts (sort, keep
+// k) when the scratch fills, and writes the final best-first k_out.
+//   loader 0: the fused kernel's per-(row, split) candidate buffers; the
+//             shared threshold gthr[row] is a lower bound of the final k-th
+//             composite, so everything below it is dropped on load.
+//   loader 1: gathered per-shard (idx, score) lists [M][S][k_in] (multi-GPU).
+// ===========================================================================
+__device__ int merge_compact(u64 *scr, int cnt, int k, int P, u64 *T, int lane) {
+  for (int i = cnt + lane; i < P; i += 64) scr[i] = 0ull;
+  wave_sync();
+  wave_sort_desc_u64(scr, P, lane);
+  if (cnt >= k) {
+    const u64 t = scr[k - 1];
+    if (t > *T) *T = t;
+    cnt = k;
+  }
+  wave_sync();
+  return cnt;
+}
+
+template <int LOADER>
+__global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wpb = blockDim.x >> 6;
+  const int row = blockIdx.x * wpb + wid;
+  if (row >= a.M) return;  // whole wave exits; no block-wide barriers below
+  u64 *scr = (u64 *)smem + (size_t)wid * a.P;
+  u64 T = (LOADER == 0) ? a.gthr[row] : 0ull;
+  int cnt = 0;
+  for (int s = 0; s < a.S; s++) {
+    const int n_s = (LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + s] : a.k_in;
+    const int64_t seg = (int64_t)row * a.S + s;
+    for (int i0 = 0; i0 < n_s; i0 += 64) {
+      const int i = i0 + lane;
+      u64 x = 0ull;
+      if (i < n_s) {
+        if (LOADER == 0) {
+          x = a.cand[seg * a.capg + i];
+        } else {
+          const uint32_t id = a.in_idx[seg * a.k_in + i];
+          const float sc = a.in_score[seg * a.k_in + i];
+          if (id != 0xFFFFFFFFu)
+            x = ((u64)okey32(a.metric == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~id);
+        }
+      }
+      const bool keep = (x != 0ull) && (x >= T);
+      const u64 m = __ballot(keep);
+      const int pos = cnt + lanes_below(m);
+      if (keep) scr[pos] = x;
+      cnt += __popcll(m);
+      if (cnt > a.P - 64) {
+        wave_sync();
+        cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
+      }
+    }
+  }
+  wave_sync();
+  const int P2 = min(a.P, next_pow2_dev(cnt));
+  for (int i = cnt + lane; i < P2; i += 64) scr[i] = 0ull;
+  wave_sync();
+  wave_sort_desc_u64(scr, P2, lane);
+  for (int j = lane; j < a.k_out; j += 64) {
+    const u64 x = (j < cnt) ? scr[j] : 0ull;
+    uint32_t id = 0xFFFFFFFFu;
+    float sc = __uint_as_float(0x7FC00000u);
+    if (x != 0ull) {
+      id = (~(uint32_t)x) + (LOADER == 0 ? a.index_base : 0u);
+      const float v = dekey32((uint32_t)(x >> 32));
+      sc = (a.metric == kMetricEuclidean) ? -v : v;
+    }
+    a.out_idx[(int64_t)row * a.k_out + j] = id;
+    a.out_score[(int64_t)row * a.k_out + j] = sc;
+  }
+}
+
+size_t merge_lds_bytes_per_wave(int P) { return (size_t)P * 8; }
+
+hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s) {
+  if (a.M <= 0) return hipSuccess;
+  int wpb = (int)(65536 / merge_lds_bytes_per_wave(a.P));
+  wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
+  const size_t lds = (size_t)wpb * merge_lds_bytes_per_wave(a.P);
+  const unsigned grid = (unsigned)((a.M + wpb - 1) / wpb);
+  if (loader == 0) merge_kernel<0><<<grid, wpb * 64, lds, s>>>(a);
+  else merge_kernel<1><<<grid, wpb * 64, lds, s>>>(a);
+  return hipGetLastError();
+}
+
+// ===========================================================================
+// f64 GEMM (store mode) on v_mfma_f64_16x16x4_f64, for the f64 path
+// (src/metrics.rs:40-157, 258-311).  64x64 tile per 4-wave workgroup, each
+// wave 32x32 = 2x2 MFMA tiles; fragments load straight from global (L2).
+// C/D layout of the f64 MFMA: col = lane&15, row = (lane>>4) + 4*reg.
+// ===========================================================================
+template <int METRIC, int XF>
+__global__ __launch_bounds__(256) void gemm_f64_kernel(const double *__restrict__ q, int64_t ldq,
+                                                       const double *__restrict__ c, int64_t ldc,
+                                                       const double *__restrict__ qn,
+                                                       const double *__restrict__ cn, int M, int N,
+                                                       int D, double *__restrict__ out,
+                                                       int64_t ldo) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  const int row0 = blockIdx.y * 64 + (wid >> 1) * 32;
+  const int col0 = blockIdx.x * 64 + (wid & 1) * 32;
+  const double *ap[2], *bp[2];
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    ap[t] = q + (int64_t)min(row0 + 16 * t + i, M - 1) * ldq + 4 * kq;
+    bp[t] = c + (int64_t)min(col0 + 16 * t + i, N - 1) * ldc + 4 * kq;
+  }
+  f64x4 acc[2][2];
+#pragma unroll
+  for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+    for (int tj = 0; tj < 2; tj++) acc[ti][tj] = (f64x4){};
+  for (int k0 = 0; k0 < D; k0 += 16) {
+    f64x2 av[2][2], bv[2][2];
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      av[t][0] = *(const f64x2 *)(ap[t] + k0);
+      av[t][1] = *(const f64x2 *)(ap[t] + k0 + 2);
+      bv[t][0] = *(const f64x2 *)(bp[t] + k0);
+      bv[t][1] = *(const f64x2 *)(bp[t] + k0 + 2);
+    }
+#pragma unroll
+    for (int st = 0; st < 4; st++)
+#pragma unroll
+      for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+        for (int tj = 0; tj < 2; tj++)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti][st >> 1][st & 1],
+                                                              bv[tj][st >> 1][st & 1],
+                                                              acc[ti][tj], 0, 0, 0);
+  }
+#pragma unroll
+  for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+    for (int tj = 0; tj < 2; tj++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int grow = row0 + 16 * ti + kq + 4 * r;
+        const int gcol = col0 + 16 * tj + i;
+        if (grow < M && gcol < N) {
+          const double v = acc[ti][tj][r];
+          out[(int64_t)grow * ldo + gcol] =
+              XF ? exact_score_f64<METRIC>(v, qn[grow], cn[gcol]) : v;
+        }
+      }
+}
+
+hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, int64_t ldc,
+                                 const double *qn, const double *cn, int M, int N, int D,
+                                 int metric, int store_metric, double *out, int64_t ldo,
+                                 hipStream_t s) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const dim3 grid((N + 63) / 64, (M + 63) / 64), blk(256);
+  if (!store_metric || metric == kMetricDot)
+    gemm_f64_kernel<kMetricDot, 0><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
+  else if (metric == kMetricCosine)
+    gemm_f64_kernel<kMetricCosine, 1><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
+  else
+    gemm_f64_kernel<kMetricEuclidean, 1><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
+  return hipGetLastError();
+}
+
+// ===========================================================================
+// Row-select over materialised (metric-transformed) scores: one wave per row
+// streams N scores, keeps entries better than the running k-th in LDS,
+// compacts when full.  src/topk.rs:6-75 semantics with the total order above.
+// ===========================================================================
+template <typename T>
+__device__ __forceinline__ u64 score_key(T v, int metric);
+template <>
+__device__ __forceinline__ u64 score_key<float>(float v, int metric) {
+  return (u64)okey32(metric == kMetricEuclidean ? -v : v);
+}
+template <>
+__device__ __forceinline__ u64 score_key<double>(double v, int metric) {
+  return okey64(metric == kMetricEuclidean ? -v : v);
+}
+template <typename T>
+__device__ __forceinline__ T key_score(u64 k, int metric);
+template <>
+__device__ __forceinline__ float key_score<float>(u64 k, int metric) {
+  const float v = dekey32((uint32_t)k);
+  return metric == kMetricEuclidean ? -v : v;
+}
+template <>
+__device__ __forceinline__ double key_score<double>(u64 k, int metric) {
+  const double v = dekey64(k);
+  return metric == kMetricEuclidean ? -v : v;
+}
+
+__device__ int ent_compact(Ent *scr, int cnt, int k, int P, Ent *Tv, bool *tfull, int lane) {
+  for (int i = cnt + lane; i < P; i += 64) scr[i] = Ent{0ull, 0xFFFFFFFFu, 0u};
+  wave_sync();
+  wave_sort_desc_ent(scr, P, lane);
+  if (cnt >= k) {
+    *Tv = scr[k - 1];
+    *tfull = true;
+    cnt = k;
+  }
+  wave_sync();
+  return cnt;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void rowselect_kernel(RowSelArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wpb = blockDim.x >> 6;
+  const int row = blockIdx.x * wpb + wid;
+  if (row >= a.rows) return;
+  Ent *scr = (Ent *)smem + (size_t)wid * a.P;
+  const T *src = (const T *)a.scores + (int64_t)row * a.lds;
+  Ent Tv{0ull, 0xFFFFFFFFu, 0u};
+  bool tfull = false;
+  int cnt = 0;
+  for (int i0 = 0; i0 < a.N; i0 += 64) {
+    const int j = i0 + lane;
+    Ent x{0ull, 0xFFFFFFFFu, 0u};
+    bool keep = false;
+    if (j < a.N) {
+      x.key = score_key<T>(src[j], a.metric);
+      x.idx = (uint32_t)j;
+      keep = !tfull || ent_better(x, Tv);
+    }
+    const u64 m = __ballot(keep);
+    const int pos = cnt + lanes_below(m);
+    if (keep) scr[pos] = x;
+    cnt += __popcll(m);
+    if (cnt > a.P - 64) {
+      wave_sync();
+      cnt = ent_compact(scr, cnt, a.k, a.P, &Tv, &tfull, lane);
+    }
+  }
+  wave_sync();
+  const int P2 = min(a.P, next_pow2_dev(cnt));
+  for (int i = cnt + lane; i < P2; i += 64) scr[i] = Ent{0ull, 0xFFFFFFFFu, 0u};
+  wave_sync();
+  wave_sort_desc_ent(scr, P2, lane);
+  T *os = (T *)a.out_score;
+  for (int j = lane; j < a.k; j += 64) {
+    const Ent x = scr[j];
+    a.out_idx[(int64_t)row * a.k + j] = x.idx + a.index_base;
+    os[(int64_t)row * a.k + j] = key_score<T>(x.key, a.metric);
+  }
+}
+
+hipError_t launch_rowselect(const RowSelArgs &a, hipStream_t s) {
+  if (a.rows <= 0) return hipSuccess;
+  const size_t per_wave = (size_t)a.P * sizeof(Ent);
+  int wpb = (int)(65536 / per_wave);
+  wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
+  const size_t lds = (size_t)wpb * per_wave;
+  const unsigned grid = (unsigned)((a.rows + wpb - 1) / wpb);
+  if (a.is_f64) rowselect_kernel<double><<<grid, wpb * 64, lds, s>>>(a);
+  else rowselect_kernel<float><<<grid, wpb * 64, lds, s>>>(a);
+  return hipGetLastError();
+}
+
+// ===========================================================================
+// Full-row global bitonic sort (k too large for the LDS row-select):
+// build entries, log^2 stage launches, extract the best k.
+// ===========================================================================
+template <typename T>
+__global__ void rowsort_build(const T *__restrict__ scores, int64_t lds, int rows, int N, int P2,
+                              int metric, Ent *__restrict__ keys) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)rows * P2) return;
+  const int r = (int)(t / P2), j = (int)(t % P2);
+  Ent e{0ull, 0xFFFFFFFFu, 0u};
+  if (j < N) {
+    e.key = score_key<T>(scores[(int64_t)r * lds + j], metric);
+    e.idx = (uint32_t)j;
+  }
+  keys[t] = e;
+}
+__global__ void rowsort_step(Ent *keys, int rows, int P2, int size, int stride) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t half = (int64_t)P2 >> 1;
+  if (t >= (int64_t)rows * half) return;
+  const int r = (int)(t / half), i = (int)(t % half);
+  const int x0 = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
+  const int x1 = x0 + stride;
+  Ent *base = keys + (int64_t)r * P2;
+  const Ent a = base[x0], b = base[x1];
+  const bool desc = (x0 & size) == 0;
+  if (desc ? ent_better(b, a) : ent_better(a, b)) {
+    base[x0] = b;
+    base[x1] = a;
+  }
+}
+template <typename T>
+__global__ void rowsort_extract(const Ent *__restrict__ keys, int rows, int P2, int k, int metric,
+                                uint32_t index_base, uint32_t *__restrict__ out_idx,
+                                T *__restrict__ out_score) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)rows * k) return;
+  const int r = (int)(t / k), j = (int)(t % k);
+  const Ent e = keys[(int64_t)r * P2 + j];
+  out_idx[t] = e.idx + index_base;
+  out_score[t] = key_score<T>(e.key, metric);
+}
+
+hipError_t launch_rowsort_global(const void *scores, int64_t lds, int rows, int N, int is_f64,
+                                 int metric, void *keys_ws, int P2, int k, uint32_t index_base,
+                                 uint32_t *out_idx, void *out_score, hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  Ent *keys = (Ent *)keys_ws;
+  const int64_t tot = (int64_t)rows * P2;
+  const unsigned gb = (unsigned)((tot + 255) / 256);
+  if (is_f64) rowsort_build<double><<<gb, 256, 0, s>>>((const double *)scores, lds, rows, N, P2, metric, keys);
+  else rowsort_build<float><<<gb, 256, 0, s>>>((const float *)scores, lds, rows, N, P2, metric, keys);
+  const unsigned gs = (unsigned)((tot / 2 + 255) / 256);
+  for (int size = 2; size <= P2; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1)
+      rowsort_step<<<gs, 256, 0, s>>>(keys, rows, P2, size, stride);
+  const int64_t tk = (int64_t)rows * k;
+  const unsigned ge = (unsigned)((tk + 255) / 256);
+  if (is_f64) rowsort_extract<double><<<ge, 256, 0, s>>>(keys, rows, P2, k, metric, index_base, out_idx, (double *)out_score);
+  else rowsort_extract<float><<<ge, 256, 0, s>>>(keys, rows, P2, k, metric, index_base, out_idx, (float *)out_score);
+  return hipGetLastError();
+}
+
+}  // namespace pmm

@@ -1,0 +1,193 @@
+"""ctypes binding of ``libpmm.so`` (the C ABI declared in ``include/pmm.h``).
+
+The reference binds its numerics through pyo3 (src/lib.rs:15-62); this module
+is the equivalent binding for the HIP library.  ctypes releases the GIL for
+the duration of every foreign call, as ``py.detach`` does in src/lib.rs:25/45.
+
+There is no CPU fallback: if ``libpmm.so`` is missing, importing this module
+raises ImportError; if no gfx950 device is visible, every compute call raises
+RuntimeError with the library's message.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpmm.so")
+
+PMM_OK = 0
+PMM_ERR_ARG = 1
+PMM_ERR_HIP = 2
+PMM_ERR_UNSUPPORTED = 3
+PMM_ERR_NODEVICE = 4
+
+METRIC_COSINE = 0
+METRIC_DOT = 1
+METRIC_EUCLIDEAN = 2
+
+COMPUTE_F32 = 0
+COMPUTE_BF16 = 1
+
+# Every symbol include/pmm.h declares (checked by tests/test_boundary.py).
+EXPORTED_SYMBOLS = (
+    "pmm_version",
+    "pmm_last_error",
+    "pmm_metric_from_str",
+    "pmm_metric_higher_is_better",
+    "pmm_device_count",
+    "pmm_set_device",
+    "pmm_topk_f32",
+    "pmm_topk_f32_ex",
+    "pmm_topk_f64",
+    "pmm_matmul_f32",
+    "pmm_matmul_f64",
+    "pmm_topk_workspace_bytes",
+    "pmm_topk_f32_device",
+    "pmm_merge_topk_device",
+    "pmm_timing_enable",
+    "pmm_timing_reset",
+    "pmm_timing_read",
+)
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"polars_matmul: HIP library not built ({LIB_PATH} missing). "
+        "Run `make -C polars-matmul_amd` or `python -c 'import __graft_entry__ as g; g.build()'`."
+    )
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+_vp, _i64, _i32, _sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_size_t
+_u32 = ctypes.c_uint32
+
+_SIGS = {
+    "pmm_version": ([], ctypes.c_char_p),
+    "pmm_last_error": ([], ctypes.c_char_p),
+    "pmm_metric_from_str": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)], _i32),
+    "pmm_metric_higher_is_better": ([_i32], _i32),
+    "pmm_device_count": ([ctypes.POINTER(ctypes.c_int)], _i32),
+    "pmm_set_device": ([_i32], _i32),
+    "pmm_topk_f32": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
+    "pmm_topk_f32_ex": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _i32, _vp, _vp], _i32),
+    "pmm_topk_f64": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
+    "pmm_matmul_f32": ([_vp, _i64, _vp, _i64, _i64, _vp], _i32),
+    "pmm_matmul_f64": ([_vp, _i64, _vp, _i64, _i64, _vp], _i32),
+    "pmm_topk_workspace_bytes": ([_i64, _i64, _i64, _i64, _i32, _i32], _sz),
+    "pmm_topk_f32_device": (
+        [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _u32, _vp, _vp, _vp, _sz, _vp],
+        _i32,
+    ),
+    "pmm_merge_topk_device": ([_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp], _i32),
+    "pmm_timing_enable": ([_i32], _i32),
+    "pmm_timing_reset": ([], _i32),
+    "pmm_timing_read": (
+        [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int64)],
+        _i32,
+    ),
+}
+for _name, (_args, _res) in _SIGS.items():
+    _fn = getattr(_lib, _name)
+    _fn.argtypes = _args
+    _fn.restype = _res
+
+
+def lib() -> ctypes.CDLL:
+    return _lib
+
+
+class PmmError(RuntimeError):
+    """A failing libpmm call; ``code`` is the PMM_ERR_* value."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+def last_error() -> str:
+    return (_lib.pmm_last_error() or b"").decode(errors="replace")
+
+
+def check(rc: int) -> None:
+    if rc != PMM_OK:
+        raise PmmError(rc, last_error())
+
+
+def ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def version() -> str:
+    return _lib.pmm_version().decode()
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    check(_lib.pmm_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def metric_from_str(s: str) -> int:
+    out = ctypes.c_int(-1)
+    check(_lib.pmm_metric_from_str(s.encode(), ctypes.byref(out)))
+    return out.value
+
+
+def topk_host(q: np.ndarray, c: np.ndarray, k: int, metric: int, compute: int = COMPUTE_F32):
+    """Host-buffer top-k.  q: (m, d), c: (n, d) C-contiguous, both f32 or both f64;
+    0 <= k <= n.  Returns (idx uint32 (m, k), scores (m, k) in the input dtype)."""
+    m, d = q.shape
+    n = c.shape[0]
+    idx = np.empty((m, k), dtype=np.uint32)
+    sc = np.empty((m, k), dtype=q.dtype)
+    if q.dtype == np.float32:
+        rc = _lib.pmm_topk_f32_ex(ptr(q), m, ptr(c), n, d, k, metric, compute, ptr(idx), ptr(sc))
+    else:
+        rc = _lib.pmm_topk_f64(ptr(q), m, ptr(c), n, d, k, metric, ptr(idx), ptr(sc))
+    check(rc)
+    return idx, sc
+
+
+def matmul_host(q: np.ndarray, c: np.ndarray) -> np.ndarray:
+    m, d = q.shape
+    n = c.shape[0]
+    out = np.empty((m, n), dtype=q.dtype)
+    fn = _lib.pmm_matmul_f32 if q.dtype == np.float32 else _lib.pmm_matmul_f64
+    check(fn(ptr(q), m, ptr(c), n, d, ptr(out)))
+    return out
+
+
+def topk_device(q_ptr: int, ldq: int, m: int, c_ptr: int, ldc: int, n: int, d: int, k: int,
+                metric: int, out_idx_ptr: int, out_score_ptr: int, *, index_base: int = 0,
+                compute: int = COMPUTE_F32, workspace: int = 0, workspace_bytes: int = 0,
+                stream: int = 0) -> None:
+    """Device-resident fused top-k (pointers are HBM addresses, e.g. torch data_ptr())."""
+    check(_lib.pmm_topk_f32_device(q_ptr, ldq, m, c_ptr, ldc, n, d, k, metric, compute,
+                                   index_base, out_idx_ptr, out_score_ptr, workspace or None,
+                                   workspace_bytes, stream or None))
+
+
+def merge_device(idx_ptr: int, score_ptr: int, m: int, lists: int, k_in: int, k_out: int,
+                 metric: int, out_idx_ptr: int, out_score_ptr: int, stream: int = 0) -> None:
+    check(_lib.pmm_merge_topk_device(idx_ptr, score_ptr, m, lists, k_in, k_out, metric,
+                                     out_idx_ptr, out_score_ptr, stream or None))
+
+
+def workspace_bytes(m: int, n: int, d: int, k: int, metric: int, compute: int = COMPUTE_F32) -> int:
+    return int(_lib.pmm_topk_workspace_bytes(m, n, d, k, metric, compute))
+
+
+def timing_enable(on: bool = True) -> None:
+    check(_lib.pmm_timing_enable(1 if on else 0))
+
+
+def timing_reset() -> None:
+    check(_lib.pmm_timing_reset())
+
+
+def timing_read(kernel: str):
+    ms = ctypes.c_double(0.0)
+    n = ctypes.c_int64(0)
+    check(_lib.pmm_timing_read(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value

@@ -1,0 +1,193 @@
+"""CPU tests of the drop-in boundary: libpmm.so loads and exports every symbol
+include/pmm.h declares; the host-side mirror of the reference's extension
+functions (input extraction, dtype dispatch, error texts and edge rules of
+src/matmul.rs / src/lib.rs) behaves as the reference does before any device
+work is issued.  No compute calls without a GPU."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pyarrow as pa
+import pytest
+
+import polars_matmul
+from polars_matmul import _native
+from polars_matmul._polars_matmul import PanicException, _matmul, _series_to_matrix, _topk
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pmm.h")
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pmm_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_symbols_match_binding_list():
+    assert header_symbols() == sorted(_native.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_header_symbol():
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    for name in header_symbols():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    for name in header_symbols():
+        assert re.search(rf"\bT {name}\b", out), f"{name} not exported"
+
+
+def test_library_targets_gfx950_only():
+    # the code objects embedded in libpmm.so are gfx950 only (no dual paths)
+    blob = open(_native.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}, targets
+
+
+def test_version_and_metric_parse_via_c_abi():
+    assert _native.version().startswith("0.1.4")
+    assert _native.metric_from_str("cosine") == _native.METRIC_COSINE
+    assert _native.metric_from_str("COSINE") == _native.METRIC_COSINE
+    assert _native.metric_from_str("dot") == _native.METRIC_DOT
+    assert _native.metric_from_str("euclidean") == _native.METRIC_EUCLIDEAN
+    assert _native.metric_from_str("l2") == _native.METRIC_EUCLIDEAN
+    with pytest.raises(_native.PmmError) as ei:
+        _native.metric_from_str("invalid_metric")
+    # src/metrics.rs:25
+    assert str(ei.value) == "Unknown metric: 'invalid_metric'. Supported: cosine, dot, euclidean"
+    assert _native.lib().pmm_metric_higher_is_better(_native.METRIC_EUCLIDEAN) == 0
+    assert _native.lib().pmm_metric_higher_is_better(_native.METRIC_COSINE) == 1
+
+
+def L(rows, t=pa.float64()):
+    return pa.array(rows, type=pa.list_(t))
+
+
+# ---- error texts / edge rules checked before any device call ----
+
+def test_topk_empty_query_returns_empty_typed():
+    # src/matmul.rs:480-487 (checked before the metric, so even a bad metric passes)
+    out = _topk(L([]), L([[1.0, 0.0]]), 1, "not_a_metric")
+    assert len(out) == 0
+    assert out.type == pa.large_list(pa.struct([("index", pa.uint32()), ("score", pa.float64())]))
+
+
+def test_topk_unknown_metric():
+    with pytest.raises(RuntimeError, match="Unknown metric"):
+        _topk(L([[1.0, 0.0]]), L([[1.0, 0.0]]), 1, "invalid_metric")
+
+
+def test_topk_empty_corpus():
+    # tests/test_polars_matmul.py:335-343
+    with pytest.raises(RuntimeError, match="Empty"):
+        _topk(L([[1.0, 0.0]]), L([]), 1, "cosine")
+
+
+def test_topk_dimension_mismatch():
+    # tests/test_polars_matmul.py:355-363
+    with pytest.raises(RuntimeError, match="Dimension mismatch: left has 2 dimensional vectors, right has 3"):
+        _topk(L([[1.0, 2.0]]), L([[1.0, 2.0, 3.0]]), 1, "cosine")
+
+
+def test_matmul_dimension_mismatch():
+    # tests/test_polars_matmul.py:345-353
+    with pytest.raises(RuntimeError, match="Dimension mismatch"):
+        _matmul(L([[1.0, 2.0]]), L([[1.0, 2.0, 3.0]]))
+
+
+def test_matmul_empty_left_is_empty_list():
+    # src/matmul.rs:297-305: empty List (not Array), f32 iff both f32
+    out = _matmul(L([], pa.float32()), L([[1.0]], pa.float32()))
+    assert len(out) == 0 and out.type == pa.large_list(pa.float32())
+    out = _matmul(L([], pa.float32()), L([[1.0]]))
+    assert out.type == pa.large_list(pa.float64())
+
+
+def test_negative_k_overflow_and_type_errors():
+    with pytest.raises(OverflowError):
+        _topk(L([[1.0]]), L([[1.0]]), -1, "cosine")
+    with pytest.raises(TypeError):
+        _topk(L([[1.0]]), L([[1.0]]), 1.5, "cosine")
+    with pytest.raises(TypeError):
+        _topk(L([[1.0]]), L([[1.0]]), 1, 3)
+
+
+def test_first_element_null_and_zero_dim():
+    with pytest.raises(RuntimeError, match="First element is null"):
+        _topk(L([None, [1.0]]), L([[1.0]]), 1, "dot")
+    with pytest.raises(RuntimeError, match="Zero-dimensional vectors"):
+        _topk(L([[]]), L([[1.0]]), 1, "dot")
+    with pytest.raises(RuntimeError, match="Zero-dimensional vectors"):
+        _topk(pa.array([[]], type=pa.list_(pa.float32(), 0)), L([[1.0]]), 1, "dot")
+
+
+def test_longer_row_panics():
+    # src/matmul.rs:276-283: d from row 0, a longer row indexes out of bounds
+    with pytest.raises(PanicException):
+        _topk(L([[1.0, 2.0], [1.0, 2.0, 3.0]]), L([[1.0, 2.0]]), 1, "dot")
+
+
+# ---- extraction (src/matmul.rs:131-286) ----
+
+def test_extract_list_with_nulls_and_short_rows():
+    arr = pa.array([[1.0, 2.0, 3.0], None, [4.0, None], [5.0, 6.0, 7.0]], type=pa.list_(pa.float64()))
+    m = _series_to_matrix(arr, np.float64)
+    assert m.tolist() == [[1.0, 2.0, 3.0], [0.0, 0.0, 0.0], [4.0, 0.0, 0.0], [5.0, 6.0, 7.0]]
+
+
+def test_extract_sliced_large_list_and_chunked():
+    arr = pa.array([[9.0, 9.0], [1.0, 2.0], [3.0, 4.0]], type=pa.large_list(pa.float32())).slice(1)
+    assert _series_to_matrix(arr, np.float32).tolist() == [[1.0, 2.0], [3.0, 4.0]]
+    ch = pa.chunked_array([pa.array([[1.0, 2.0]], type=pa.list_(pa.float32())),
+                           pa.array([[3.0, 4.0]], type=pa.list_(pa.float32()))])
+    from polars_matmul._polars_matmul import _to_arrow
+    assert _series_to_matrix(_to_arrow(ch), np.float32).tolist() == [[1.0, 2.0], [3.0, 4.0]]
+
+
+def test_extract_fixed_size_list_zero_copy_and_slice():
+    base = np.arange(24, dtype=np.float32)
+    arr = pa.FixedSizeListArray.from_arrays(pa.array(base), 4)
+    m = _series_to_matrix(arr, np.float32)
+    assert m.shape == (6, 4) and m.dtype == np.float32
+    assert np.shares_memory(m, np.asarray(arr.values)) or m.flags.c_contiguous
+    s = arr.slice(2, 3)
+    assert _series_to_matrix(s, np.float32).tolist() == base.reshape(6, 4)[2:5].tolist()
+    # f32 Array into the f64 path is cast
+    assert _series_to_matrix(s, np.float64).dtype == np.float64
+
+
+def test_extract_fixed_size_list_null_rows_are_zero():
+    arr = pa.array([[1.0, 2.0], None, [3.0, 4.0]], type=pa.list_(pa.float64(), 2))
+    assert _series_to_matrix(arr, np.float64).tolist() == [[1.0, 2.0], [0.0, 0.0], [3.0, 4.0]]
+
+
+def test_dtype_dispatch_rules():
+    from polars_matmul._polars_matmul import _is_f32
+    assert _is_f32(pa.array([[1.0]], type=pa.list_(pa.float32())))
+    assert _is_f32(pa.array([[1.0]], type=pa.list_(pa.float32(), 1)))
+    assert not _is_f32(pa.array([[1.0]], type=pa.list_(pa.float64())))
+    assert not _is_f32(pa.array([[1]], type=pa.list_(pa.int64())))
+    # ints go through the f64 path with a cast (src/matmul.rs:143)
+    m = _series_to_matrix(pa.array([[1, 2]], type=pa.list_(pa.int64())), np.float64)
+    assert m.dtype == np.float64 and m.tolist() == [[1.0, 2.0]]
+
+
+def test_compute_fails_loudly_without_device():
+    if _native.device_count() > 0:
+        pytest.skip("a GPU is visible: covered by the gpu tests")
+    with pytest.raises(RuntimeError):
+        _topk(L([[1.0, 0.0]]), L([[1.0, 0.0]]), 1, "cosine")
+    with pytest.raises(RuntimeError):
+        polars_matmul.matmul(np.ones((2, 2)), np.ones((2, 2)))
+
+
+def test_pmm_namespace_placeholder_without_polars():
+    try:
+        import polars  # noqa: F401
+    except Exception:
+        with pytest.raises(ImportError):
+            polars_matmul.PmmNamespace(None)
