@@ -102,7 +102,8 @@ int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64
 
 /* ---------------------------------------------------------------------------
  * Device-resident entry points: inputs already in HBM, work enqueued on the
- * caller's HIP stream (NULL = this thread's stream), no host synchronisation.
+ * caller's HIP stream (NULL = the HIP default stream, as in the HIP API), no
+ * host synchronisation.
  * Used by the benchmark and the multi-GPU (corpus-sharded) path.
  * ------------------------------------------------------------------------- */
 
@@ -114,7 +115,7 @@ size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int 
  * d must be a multiple of 32 and ldq/ldc multiples of 4 with 16-byte-aligned
  * bases (pmm_topk_f32 pads host inputs itself).  index_base is added to every
  * returned corpus index (global index of corpus row 0 of this shard).
- * workspace may be NULL (allocated stream-ordered and cached per thread). */
+ * workspace may be NULL (a per-thread cached buffer is used). */
 int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, int64_t ldc,
                         int64_t n, int64_t d, int64_t k, int metric, int compute,
                         uint32_t index_base, uint32_t *out_idx, float *out_score,

@@ -505,8 +505,7 @@ int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, 
                 (long long)d, (long long)ldq, (long long)ldc);
   int dev;
   if ((rc = ensure_device(&dev))) return rc;
-  hipStream_t s = (hipStream_t)stream;
-  if (!s && (rc = thread_stream(dev, &s))) return rc;
+  hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream
   return topk_f32_device_impl(q, ldq, m, c, ldc, n, d, k, metric, index_base, out_idx, out_score,
                               workspace, workspace_bytes, s, dev);
 }
@@ -690,8 +689,7 @@ int pmm_merge_topk_device(const uint32_t *idx, const float *score, int64_t m, in
   if (m == 0 || k_out == 0) return PMM_OK;
   int dev;
   if ((rc = ensure_device(&dev))) return rc;
-  hipStream_t s = (hipStream_t)stream;
-  if (!s && (rc = thread_stream(dev, &s))) return rc;
+  hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream
   MergeArgs ma{};
   ma.in_idx = idx;
   ma.in_score = score;

@@ -51,6 +51,17 @@ EXPORTED_SYMBOLS = (
     "pmm_timing_read",
 )
 
+if os.environ.get("PMM_NO_TORCH_PRELOAD") != "1":
+    # PyTorch-ROCm ships its own libamdhip64.so (same SONAME as /opt/rocm's).
+    # Whichever loads first wins the SONAME; if libpmm.so pulled in /opt/rocm's
+    # runtime before torch, torch would load a second HIP runtime and find no
+    # devices.  Loading torch first makes the whole process share one runtime,
+    # so torch tensors (device memory, streams) can be passed to the C ABI.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
 if not os.path.exists(LIB_PATH):
     raise ImportError(
         f"polars_matmul: HIP library not built ({LIB_PATH} missing). "
