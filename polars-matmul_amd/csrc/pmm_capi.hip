@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -165,14 +166,16 @@ struct Timed {
 // memory budget (M * S * capg * 8 bytes).
 // ---------------------------------------------------------------------------
 struct Plan {
+  int variant = 0;
   int QB = 0, T = 0, tps = 0, S = 0, units = 0, grid = 0, capg = 0, P = 0;
   size_t off_counter = 0, off_gthr = 0, off_cnt = 0, off_cand = 0, off_qn = 0, off_cn = 0;
   size_t total = 0;
 };
 
-void plan_units(int64_t m, int64_t n, int cus, double unit_overhead, int64_t max_S, Plan &p) {
-  p.QB = (int)cdiv(m, gemm_f32_bm());
-  p.T = (int)cdiv(n, gemm_f32_bn());
+void plan_units(int64_t m, int64_t n, int bm, int bn, int cus, double unit_overhead, int64_t max_S,
+                Plan &p) {
+  p.QB = (int)cdiv(m, bm);
+  p.T = (int)cdiv(n, bn);
   double best = 1e300;
   int best_tps = p.T;
   for (int tps = 1; tps <= p.T; tps++) {
@@ -193,12 +196,29 @@ void plan_units(int64_t m, int64_t n, int cus, double unit_overhead, int64_t max
   p.grid = (int)std::min<int64_t>(p.units, cus);
 }
 
+// Tile-shape variant: PMM_GEMM_VARIANT overrides; otherwise the preferred
+// order below, skipping variants whose LDS (staging + per-wave scratch) does
+// not fit in the CU's 160 KiB.
+int choose_variant(int mode, int capg) {
+  static int env = -2;
+  if (env == -2) {
+    const char *e = getenv("PMM_GEMM_VARIANT");
+    env = e ? atoi(e) : -1;
+  }
+  if (env >= 0 && env < 4 && gemm_f32_lds_bytes(env, mode, capg) <= 160 * 1024) return env;
+  static const int order[4] = {0, 1, 2, 3};
+  for (int v : order)
+    if (gemm_f32_lds_bytes(v, mode, capg) <= 160 * 1024) return v;
+  return 0;
+}
+
 int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p) {
   p.capg = next_pow2((int)k + 64, 128);
+  p.variant = choose_variant(0, p.capg);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
   const size_t cand_budget = size_t(8) << 30;
   int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
-  plan_units(m, n, cus, 0.5, max_S, p);
+  plan_units(m, n, gemm_f32_bm(p.variant), gemm_f32_bn(p.variant), cus, 0.5, max_S, p);
   p.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
   size_t off = 0;
   p.off_counter = off;
@@ -257,7 +277,8 @@ int gemm_store_f32(const float *q, int64_t ldq, int64_t rows, const float *c, in
                    int64_t d, int metric, int store_metric, const float *qn, const float *cn,
                    float *out, int64_t ldo, unsigned *counter, int cus, hipStream_t s) {
   Plan p;
-  plan_units(rows, n, cus, 0.1, 1 << 20, p);
+  p.variant = choose_variant(1, 0);
+  plan_units(rows, n, gemm_f32_bm(p.variant), gemm_f32_bn(p.variant), cus, 0.1, 1 << 20, p);
   GemmF32Args a{};
   a.q = q;
   a.c = c;
@@ -282,7 +303,7 @@ int gemm_store_f32(const float *q, int64_t ldq, int64_t rows, const float *c, in
   a.store_metric = store_metric;
   HIP_TRY(hipMemsetAsync(counter, 0, 4, s));
   Timed t(store_metric ? "gemm_f32_scores" : "gemm_f32_matmul", s);
-  HIP_TRY(launch_gemm_f32(a, 1, p.grid, s));
+  HIP_TRY(launch_gemm_f32(a, p.variant, 1, p.grid, s));
   return PMM_OK;
 }
 
@@ -333,7 +354,7 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     a.gthr = (unsigned long long *)(w + p.off_gthr);
     {
       Timed t("gemm_f32_topk", s);
-      HIP_TRY(launch_gemm_f32(a, 0, p.grid, s));
+      HIP_TRY(launch_gemm_f32(a, p.variant, 0, p.grid, s));
     }
     MergeArgs ma{};
     ma.cand = a.cand;

@@ -68,11 +68,13 @@ hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld,
                             float *out, hipStream_t s);
 hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,
                             double *out, hipStream_t s);
+// Tile-shape variant of the f32 GEMM (see pmm_kernels.hip): 0 = 128x128,
+// 1 = 128x256, 2 = 256x128 (2 waves/SIMD), 3 = 256x256 (2 waves/SIMD).
 // mode 0 = fused top-k, 1 = store.  grid = number of persistent workgroups.
-hipError_t launch_gemm_f32(const GemmF32Args &a, int mode, int grid, hipStream_t s);
-int gemm_f32_bm();   // rows per workgroup
-int gemm_f32_bn();   // corpus columns per tile
-size_t gemm_f32_lds_bytes(int mode, int capg);
+hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid, hipStream_t s);
+int gemm_f32_bm(int variant);   // query rows per workgroup
+int gemm_f32_bn(int variant);   // corpus columns per tile
+size_t gemm_f32_lds_bytes(int variant, int mode, int capg);
 hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s);
 size_t merge_lds_bytes_per_wave(int P);
 hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, int64_t ldc,

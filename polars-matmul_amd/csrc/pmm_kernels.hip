@@ -251,58 +251,64 @@ __device__ __forceinline__ float prefilter_lo(u64 thr) {
 // columns); persistent workgroups pull units from a counter, split-major, so
 // the workgroups running together stream the same corpus tiles through the
 // XCD L2s.  Workgroup = NW waves; wave w owns query rows [32w, 32w+32) of the
-// block and all BN columns (NB 32x32 accumulators), so every per-row top-k
-// state has exactly one owning wave and needs no cross-wave sync.
+// block and all BN columns (NB 32x32 accumulators in AGPRs), so every per-row
+// top-k state has exactly one owning wave and needs no cross-wave sync.
 //
-// K loop (BK = 32 floats): the corpus tile is staged HBM -> LDS with
-// global_load_lds_dwordx4 (double-buffered, XOR-swizzled on the source
-// address so the ds_read_b128 fragment reads are conflict-free); each wave's
-// query fragment goes straight to VGPRs (not shared between waves).  Lane
-// (r = lane&31, h = lane>>5) covers k = 16h..16h+15 of the step, so MFMA
+// K loop (BK = 32 floats = one 128-byte row piece per operand row): both the
+// wave's query rows and the shared corpus tile are staged HBM -> LDS by
+// buffer_load ... lds (LDS-DMA, 16 B per lane, double-buffered, one barrier
+// per step).  The buffer resources carry the row range, so rows past M / N
+// read as zeros with no clamping, and each lane's byte offset is loop
+// invariant (the step advances only the scalar soffset).  The 16-byte chunks
+// of every 128-byte row are XOR-swizzled on the SOURCE address (chunk ^
+// ((row>>1)&7)) so the ds_read_b128 fragment reads hit 16 distinct bank slots.
+// Lane (r = lane&31, h = lane>>5) covers k = 16h..16h+15 of the step, so MFMA
 // substep s pairs k = s and k = 16+s (the dot product is order-free; f32
 // rounding differs from faer's order only within the stated tolerance).
 // ===========================================================================
-constexpr int NB = 4;             // 32-column MFMA blocks per wave
-constexpr int NW = 4;             // waves per workgroup
-constexpr int BN = 32 * NB;       // corpus columns per tile
-constexpr int BM = 32 * NW;       // query rows per workgroup
-constexpr int BT = BN * 128;      // bytes per staged corpus tile (BN x 32 f32)
-constexpr int GLDS_PER_WAVE = BT / 1024 / NW;
-static_assert(BT % (1024 * NW) == 0, "corpus tile must split into 1 KiB LDS-DMA pieces per wave");
+template <int NB, int NW>
+struct GemmShape {
+  static constexpr int BN = 32 * NB;                // corpus columns per tile
+  static constexpr int BM = 32 * NW;                // query rows per workgroup
+  static constexpr int A_BYTES = NW * 4096;         // NW waves x 32 rows x 128 B
+  static constexpr int B_BYTES = BN * 128;          // BN rows x 128 B
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int BPIECES = B_BYTES / 1024 / NW;  // 1 KiB LDS-DMA pieces per wave
+  static constexpr int OFF_THR = 2 * STAGE;
+  static constexpr int OFF_CNT = OFF_THR + BM * 8;
+  static constexpr int OFF_UNIT = OFF_CNT + BM * 4;
+  static constexpr int OFF_SCR = OFF_UNIT + 16;
+  static_assert(B_BYTES % (1024 * NW) == 0, "corpus tile must split into 1 KiB pieces per wave");
+  static_assert(OFF_SCR % 16 == 0, "LDS carve must stay 16-byte aligned");
+};
 
-int gemm_f32_bm() { return BM; }
-int gemm_f32_bn() { return BN; }
+// Tile-shape variants compiled in (index = GemmVariant id).
+//   0: NB=4 NW=4 (128 x 128, 1 wave/SIMD)   1: NB=8 NW=4 (128 x 256)
+//   2: NB=4 NW=8 (256 x 128, 2 waves/SIMD)  3: NB=8 NW=8 (256 x 256)
+constexpr int kGemmVariants = 4;
+constexpr int kVarNB[kGemmVariants] = {4, 8, 4, 8};
+constexpr int kVarNW[kGemmVariants] = {4, 4, 8, 8};
 
-// LDS: [B stage 0 | B stage 1 | thr[BM] u64 | cnt[BM] u32 | unit | scratch NW*capg u64]
-constexpr int LDS_OFF_THR = 2 * BT;
-constexpr int LDS_OFF_CNT = LDS_OFF_THR + BM * 8;
-constexpr int LDS_OFF_UNIT = LDS_OFF_CNT + BM * 4;
-constexpr int LDS_OFF_SCR = LDS_OFF_UNIT + 16;
-static_assert(LDS_OFF_SCR % 16 == 0, "LDS carve must stay 16-byte aligned");
+int gemm_f32_bm(int variant) { return 32 * kVarNW[variant]; }
+int gemm_f32_bn(int variant) { return 32 * kVarNB[variant]; }
 
-size_t gemm_f32_lds_bytes(int mode, int capg) {
-  return (size_t)LDS_OFF_SCR + (mode == 0 ? (size_t)NW * capg * 8 : 0);
+size_t gemm_f32_lds_bytes(int variant, int mode, int capg) {
+  const int nb = kVarNB[variant], nw = kVarNW[variant];
+  const size_t stage = (size_t)nw * 4096 + (size_t)32 * nb * 128;
+  const size_t fixed = 2 * stage + (size_t)32 * nw * 12 + 16;
+  return fixed + (mode == 0 ? (size_t)nw * capg * 8 : 0);
 }
 
 __device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
 
-__device__ __forceinline__ void stage_b(const float *__restrict__ c, int64_t ldc, int col0, int N,
-                                        int kofs, char *buf, int wid, int lane) {
-#pragma unroll
-  for (int i = 0; i < GLDS_PER_WAVE; i++) {
-    const int blk = i * NW + wid;           // 1 KiB piece = 8 corpus rows x 128 B
-    const int col = blk * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ ((col >> 1) & 7);
-    const int gcol = min(col0 + col, N - 1);
-    const float *src = c + (int64_t)gcol * ldc + kofs + ch * 4;
-    __builtin_amdgcn_global_load_lds((const GLB_AS void *)src, (LDS_AS void *)(buf + blk * 1024),
-                                     16, 0, 0);
-  }
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float *base, int64_t bytes) {
+  const int nrec = bytes <= 0 ? 0 : (int)(bytes > 0x7FFFFFFFll ? 0x7FFFFFFFll : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, nrec, 0x00020000);
 }
 
-__device__ __forceinline__ void load_a(const float *aptr, int kofs, f32x4 (&a)[4]) {
-#pragma unroll
-  for (int j = 0; j < 4; j++) a[j] = *(const f32x4 *)(aptr + kofs + 4 * j);
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *lds, uint32_t voff,
+                                      uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void *)lds, 16, voff, soff, 0, 0);
 }
 
 // Wave-level compaction of one row's candidate buffer: sort, keep the best k,
@@ -330,22 +336,43 @@ __device__ void compact_row(const GemmF32Args &a, int s, int grow, u64 *thr_slot
   wave_sync();
 }
 
-template <int MODE, int METRIC>
-__global__ __launch_bounds__(NW * 64, 1) void gemm_f32_kernel(GemmF32Args a) {
+template <int NB, int NW, int MODE, int METRIC>
+__global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a) {
+  using G = GemmShape<NB, NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char *bbuf = smem;
-  u64 *thr_l = (u64 *)(smem + LDS_OFF_THR);
-  unsigned *cnt_l = (unsigned *)(smem + LDS_OFF_CNT);
-  int *unit_l = (int *)(smem + LDS_OFF_UNIT);
+  u64 *thr_l = (u64 *)(smem + G::OFF_THR);
+  unsigned *cnt_l = (unsigned *)(smem + G::OFF_CNT);
+  int *unit_l = (int *)(smem + G::OFF_UNIT);
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r32 = lane & 31, h = lane >> 5;
   const int KS = a.D >> 5;
-  u64 *scr = (u64 *)(smem + LDS_OFF_SCR) + (size_t)wid * a.capg;
+  u64 *scr = (u64 *)(smem + G::OFF_SCR) + (size_t)wid * a.capg;
   u64 *thr_w = thr_l + wid * 32;
   unsigned *cnt_w = cnt_l + wid * 32;
   constexpr bool XFORM = (METRIC != kMetricDot);
 
+  // Loop-invariant per-lane byte offsets of this wave's LDS-DMA pieces.
+  uint32_t a_voff[4], b_voff[G::BPIECES];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int row = 8 * i + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    a_voff[i] = (uint32_t)(row * a.ldq * 4 + ch * 16);
+  }
+#pragma unroll
+  for (int i = 0; i < G::BPIECES; i++) {
+    const int col = (i * NW + wid) * 8 + (lane >> 3);
+    const int ch = (lane & 7) ^ ((col >> 1) & 7);
+    b_voff[i] = (uint32_t)(col * a.ldc * 4 + ch * 16);
+  }
+  // Per-lane LDS read offsets (within a stage).
+  const int swz = (r32 >> 1) & 7;
+  const int a_rd = wid * 4096 + r32 * 128;
+  const int b_rd = G::A_BYTES + r32 * 128;
+
+  int buf = 0;
   for (;;) {
     if (tid == 0) *unit_l = (int)atomicAdd(a.counter, 1u);
     __syncthreads();
@@ -356,9 +383,9 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_f32_kernel(GemmF32Args a) {
     const int qb = unit - s * a.QB;
     const int t0 = s * a.tps;
     const int t1 = min(t0 + a.tps, a.ntiles);
-    const int wrow0 = qb * BM + wid * 32;
-    const int arow = min(wrow0 + r32, a.M - 1);
-    const float *aptr = a.q + (int64_t)arow * a.ldq + 16 * h;
+    const int wrow0 = qb * G::BM + wid * 32;
+    const __amdgpu_buffer_rsrc_t ra =
+        make_rsrc(a.q + (int64_t)wrow0 * a.ldq, (int64_t)min(32, a.M - wrow0) * a.ldq * 4);
 
     // Per-lane row constants for the 16 accumulator rows this lane holds.
     float rv[16], lo[16];
@@ -377,9 +404,9 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_f32_kernel(GemmF32Args a) {
     if (MODE == 0) {
       if (lane < 32) {
         const int grow = wrow0 + lane;
-        thr_w[lane] = (grow < a.M)
-                          ? __hip_atomic_load(a.gthr + grow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                          : ~0ull;
+        thr_w[lane] = (grow < a.M) ? __hip_atomic_load(a.gthr + grow, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT)
+                                   : ~0ull;
         cnt_w[lane] = 0u;
       }
       wave_sync();
@@ -387,134 +414,127 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_f32_kernel(GemmF32Args a) {
       for (int e = 0; e < 16; e++) lo[e] = prefilter_lo<METRIC>(thr_w[acc_row(e, h)]);
     }
 
-    const int nsteps = (t1 - t0) * KS;
-    f32x4 acur[4], anext[4];
-    stage_b(a.c, a.ldc, t0 * BN, a.N, 0, bbuf, wid, lane);
-    load_a(aptr, 0, acur);
-    __syncthreads();
-
-    f32x16 acc[NB];
+    auto rsrc_b = [&](int tile) {
+      const int col0 = tile * G::BN;
+      return make_rsrc(a.c + (int64_t)col0 * a.ldc, (int64_t)min(G::BN, a.N - col0) * a.ldc * 4);
+    };
+    auto stage = [&](int sb, __amdgpu_buffer_rsrc_t rb, int ks) {
+      char *st = smem + sb * G::STAGE;
+      const uint32_t soff = (uint32_t)ks * 128u;
 #pragma unroll
-    for (int c = 0; c < NB; c++) acc[c] = (f32x16){};
-
-    int tile = t0, ks = 0;
-    for (int g = 0; g < nsteps; g++) {
-      int ntile = tile, nks = ks + 1;
-      if (nks == KS) {
-        nks = 0;
-        ntile++;
-      }
-      const bool more = (g + 1) < nsteps;
-      if (more) {
-        stage_b(a.c, a.ldc, ntile * BN, a.N, nks * 32, bbuf + ((g + 1) & 1) * BT, wid, lane);
-        load_a(aptr, nks * 32, anext);
-      }
-      const char *B = bbuf + (g & 1) * BT;
-      const int swz = (r32 >> 1) & 7;
+      for (int i = 0; i < 4; i++) dma16(ra, st + wid * 4096 + i * 1024, a_voff[i], soff);
 #pragma unroll
-      for (int qd = 0; qd < 4; qd++) {
-        f32x4 b[NB];
+      for (int i = 0; i < G::BPIECES; i++)
+        dma16(rb, st + G::A_BYTES + (i * NW + wid) * 1024, b_voff[i], soff);
+    };
+
+    __amdgpu_buffer_rsrc_t rb = rsrc_b(t0);
+    stage(buf, rb, 0);
+    for (int tile = t0; tile < t1; tile++) {
+      const bool last_tile = (tile + 1) >= t1;
+      const __amdgpu_buffer_rsrc_t rbn = last_tile ? rb : rsrc_b(tile + 1);
+      f32x16 acc[NB];
+#pragma unroll
+      for (int c = 0; c < NB; c++) acc[c] = (f32x16){};
+      for (int ks = 0; ks < KS; ks++) {
+        __syncthreads();  // stage `buf` landed (vmcnt(0) + barrier); buf^1 free
+        if (ks + 1 < KS) stage(buf ^ 1, rb, ks + 1);
+        else if (!last_tile) stage(buf ^ 1, rbn, 0);
+        const char *st = smem + buf * G::STAGE;
+#pragma unroll
+        for (int qd = 0; qd < 4; qd++) {
+          const int co = 16 * ((4 * h + qd) ^ swz);
+          const f32x4 av = *(const f32x4 *)(st + a_rd + co);
+          f32x4 b[NB];
+#pragma unroll
+          for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+#pragma unroll
+            for (int c = 0; c < NB; c++)
+              acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], b[c][j], acc[c], 0, 0, 0);
+          }
+        }
+        buf ^= 1;
+      }
+      rb = rbn;
+
+      const int col0 = tile * G::BN;
+      if (MODE == 1) {
+        // ---- store epilogue (.pmm.matmul, or materialised scores) ----
 #pragma unroll
         for (int c = 0; c < NB; c++) {
-          const int col = 32 * c + r32;
-          b[c] = *(const f32x4 *)(B + col * 128 + 16 * ((4 * h + qd) ^ swz));
-        }
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-#pragma unroll
-          for (int c = 0; c < NB; c++)
-            acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[qd][j], b[c][j], acc[c], 0, 0, 0);
-        }
-      }
-
-      if (ks == KS - 1) {
-        const int col0 = tile * BN;
-        if (MODE == 1) {
-          // ---- store epilogue (.pmm.matmul, or materialised scores) ----
-#pragma unroll
-          for (int c = 0; c < NB; c++) {
-            const int gcol = col0 + 32 * c + r32;
-            if (gcol < a.N) {
-              const float cv = XFORM ? a.cn[gcol] : 0.0f;
-#pragma unroll
-              for (int e = 0; e < 16; e++) {
-                const int grow = wrow0 + acc_row(e, h);
-                if (grow < a.M) {
-                  const float v = acc[c][e];
-                  a.out[(int64_t)grow * a.ldo + gcol] =
-                      (XFORM && a.store_metric) ? exact_score<METRIC>(v, rv[e], cv) : v;
-                }
-              }
-            }
-          }
-        } else {
-          // ---- fused top-k epilogue ----
-#pragma unroll
-          for (int c = 0; c < NB; c++) {
-            const int gcol = col0 + 32 * c + r32;
-            const bool cvalid = gcol < a.N;
-            const int gcc = min(gcol, a.N - 1);
-            float cv = 0.0f;
-            if (METRIC == kMetricCosine) {
-              const float x = a.cn[gcc];
-              cv = (x > 1e-6f) ? 1.0f / x : 0.0f;
-            } else if (METRIC == kMetricEuclidean) {
-              cv = a.cn[gcc];
-            }
-            bool any = false;
+          const int gcol = col0 + 32 * c + r32;
+          if (gcol < a.N) {
+            const float cv = XFORM ? a.cn[gcol] : 0.0f;
 #pragma unroll
             for (int e = 0; e < 16; e++) {
-              const float v = acc[c][e];
-              float pv;
-              if (METRIC == kMetricDot) pv = v;
-              else if (METRIC == kMetricCosine) pv = (v * rv[e]) * cv;
-              else pv = fmaf(2.0f, v, -(rv[e] + cv));
-              any |= !(pv < lo[e]);
-            }
-            any = any && cvalid;
-            if (__ballot(any) != 0ull) {
-              // exact path: rare after the first tiles of a unit
-              const float cex = XFORM ? a.cn[gcc] : 0.0f;
-#pragma unroll
-              for (int e = 0; e < 16; e++) {
-                const int rl = acc_row(e, h);
-                const int grow = wrow0 + rl;
-                const float qex = XFORM ? a.qn[min(grow, a.M - 1)] : 0.0f;
-                const float sc = exact_score<METRIC>(acc[c][e], qex, cex);
-                const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
-                const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
-                if (cvalid && comp > thr_w[rl]) {
-                  const unsigned pos = atomicAdd(&cnt_w[rl], 1u);
-                  a.cand[((int64_t)grow * a.S + s) * a.capg + pos] = comp;
-                }
-              }
-              wave_sync();
-              const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
-              u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 32));
-              if (need) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                while (need) {
-                  const int r = __builtin_ctzll(need);
-                  need &= need - 1;
-                  compact_row(a, s, wrow0 + r, thr_w + r, cnt_w + r, scr, lane);
-                }
-#pragma unroll
-                for (int e = 0; e < 16; e++) lo[e] = prefilter_lo<METRIC>(thr_w[acc_row(e, h)]);
+              const int grow = wrow0 + acc_row(e, h);
+              if (grow < a.M) {
+                const float v = acc[c][e];
+                a.out[(int64_t)grow * a.ldo + gcol] =
+                    (XFORM && a.store_metric) ? exact_score<METRIC>(v, rv[e], cv) : v;
               }
             }
           }
         }
+      } else {
+        // ---- fused top-k epilogue ----
 #pragma unroll
-        for (int c = 0; c < NB; c++) acc[c] = (f32x16){};
-      }
-
-      __syncthreads();
-      if (more) {
+        for (int c = 0; c < NB; c++) {
+          const int gcol = col0 + 32 * c + r32;
+          const bool cvalid = gcol < a.N;
+          const int gcc = min(gcol, a.N - 1);
+          float cv = 0.0f;
+          if (METRIC == kMetricCosine) {
+            const float x = a.cn[gcc];
+            cv = (x > 1e-6f) ? 1.0f / x : 0.0f;
+          } else if (METRIC == kMetricEuclidean) {
+            cv = a.cn[gcc];
+          }
+          bool any = false;
 #pragma unroll
-        for (int j = 0; j < 4; j++) acur[j] = anext[j];
+          for (int e = 0; e < 16; e++) {
+            const float v = acc[c][e];
+            float pv;
+            if (METRIC == kMetricDot) pv = v;
+            else if (METRIC == kMetricCosine) pv = (v * rv[e]) * cv;
+            else pv = fmaf(2.0f, v, -(rv[e] + cv));
+            any |= !(pv < lo[e]);
+          }
+          any = any && cvalid;
+          if (__ballot(any) != 0ull) {
+            // exact path: rare after the first tiles of a unit
+            const float cex = XFORM ? a.cn[gcc] : 0.0f;
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+              const int rl = acc_row(e, h);
+              const int grow = wrow0 + rl;
+              const float qex = XFORM ? a.qn[min(grow, a.M - 1)] : 0.0f;
+              const float sc = exact_score<METRIC>(acc[c][e], qex, cex);
+              const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
+              const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
+              if (cvalid && comp > thr_w[rl]) {
+                const unsigned pos = atomicAdd(&cnt_w[rl], 1u);
+                a.cand[((int64_t)grow * a.S + s) * a.capg + pos] = comp;
+              }
+            }
+            wave_sync();
+            const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
+            u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 32));
+            if (need) {
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              while (need) {
+                const int r = __builtin_ctzll(need);
+                need &= need - 1;
+                compact_row(a, s, wrow0 + r, thr_w + r, cnt_w + r, scr, lane);
+              }
+#pragma unroll
+              for (int e = 0; e < 16; e++) lo[e] = prefilter_lo<METRIC>(thr_w[acc_row(e, h)]);
+            }
+          }
+        }
       }
-      tile = ntile;
-      ks = nks;
     }
 
     if (MODE == 0) {
@@ -526,30 +546,43 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_f32_kernel(GemmF32Args a) {
   }
 }
 
-template <int MODE, int METRIC>
+template <int NB, int NW, int MODE, int METRIC>
 static hipError_t launch_gemm_f32_t(const GemmF32Args &a, int grid, size_t lds, hipStream_t s) {
-  static bool attr_set = false;  // opt in to > 64 KiB dynamic LDS (large k)
+  static bool attr_set = false;  // opt in to > 64 KiB dynamic LDS
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)gemm_f32_kernel<MODE, METRIC>,
+    hipError_t e = hipFuncSetAttribute((const void *)gemm_f32_kernel<NB, NW, MODE, METRIC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  gemm_f32_kernel<MODE, METRIC><<<dim3(grid), dim3(NW * 64), lds, s>>>(a);
+  gemm_f32_kernel<NB, NW, MODE, METRIC><<<dim3(grid), dim3(NW * 64), lds, s>>>(a);
   return hipGetLastError();
 }
 
-hipError_t launch_gemm_f32(const GemmF32Args &a, int mode, int grid, hipStream_t s) {
-  const size_t lds = gemm_f32_lds_bytes(mode, a.capg);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+template <int NB, int NW>
+static hipError_t launch_gemm_f32_v(const GemmF32Args &a, int mode, int grid, size_t lds,
+                                    hipStream_t s) {
   if (mode == 0) {
-    if (a.metric == kMetricCosine) return launch_gemm_f32_t<0, kMetricCosine>(a, grid, lds, s);
-    if (a.metric == kMetricDot) return launch_gemm_f32_t<0, kMetricDot>(a, grid, lds, s);
-    return launch_gemm_f32_t<0, kMetricEuclidean>(a, grid, lds, s);
+    if (a.metric == kMetricCosine) return launch_gemm_f32_t<NB, NW, 0, kMetricCosine>(a, grid, lds, s);
+    if (a.metric == kMetricDot) return launch_gemm_f32_t<NB, NW, 0, kMetricDot>(a, grid, lds, s);
+    return launch_gemm_f32_t<NB, NW, 0, kMetricEuclidean>(a, grid, lds, s);
   }
-  if (!a.store_metric || a.metric == kMetricDot) return launch_gemm_f32_t<1, kMetricDot>(a, grid, lds, s);
-  if (a.metric == kMetricCosine) return launch_gemm_f32_t<1, kMetricCosine>(a, grid, lds, s);
-  return launch_gemm_f32_t<1, kMetricEuclidean>(a, grid, lds, s);
+  if (!a.store_metric || a.metric == kMetricDot)
+    return launch_gemm_f32_t<NB, NW, 1, kMetricDot>(a, grid, lds, s);
+  if (a.metric == kMetricCosine) return launch_gemm_f32_t<NB, NW, 1, kMetricCosine>(a, grid, lds, s);
+  return launch_gemm_f32_t<NB, NW, 1, kMetricEuclidean>(a, grid, lds, s);
+}
+
+hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid, hipStream_t s) {
+  const size_t lds = gemm_f32_lds_bytes(variant, mode, a.capg);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  switch (variant) {
+    case 0: return launch_gemm_f32_v<4, 4>(a, mode, grid, lds, s);
+    case 1: return launch_gemm_f32_v<8, 4>(a, mode, grid, lds, s);
+    case 2: return launch_gemm_f32_v<4, 8>(a, mode, grid, lds, s);
+    case 3: return launch_gemm_f32_v<8, 8>(a, mode, grid, lds, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 // ===========================================================================
