@@ -206,7 +206,7 @@ int choose_variant(int mode, int capg) {
     env = e ? atoi(e) : -1;
   }
   if (env >= 0 && env < 4 && gemm_f32_lds_bytes(env, mode, capg) <= 160 * 1024) return env;
-  static const int order[4] = {0, 1, 2, 3};
+  static const int order[4] = {2, 0, 1, 3};  // measured on c3: v2 123.7, v1 105, v0 103.6 TFLOP/s
   for (int v : order)
     if (gemm_f32_lds_bytes(v, mode, capg) <= 160 * 1024) return v;
   return 0;
