@@ -206,7 +206,8 @@ int choose_variant(int mode, int capg) {
     env = e ? atoi(e) : -1;
   }
   if (env >= 0 && env < 4 && gemm_f32_lds_bytes(env, mode, capg) <= 160 * 1024) return env;
-  static const int order[4] = {2, 0, 1, 3};  // measured on c3: v2 123.7, v1 105, v0 103.6 TFLOP/s
+  // measured on c3 (100k x 1M x 768 cosine k=100): v3 136.9, v2 133.1, v1 120.5 TFLOP/s
+  static const int order[4] = {3, 2, 0, 1};
   for (int v : order)
     if (gemm_f32_lds_bytes(v, mode, capg) <= 160 * 1024) return v;
   return 0;
@@ -229,10 +230,10 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   off = al256(off + (size_t)m * p.S * 4);
   p.off_cand = off;
   off = al256(off + (size_t)m * p.S * p.capg * 8);
-  p.off_qn = off;
-  off = al256(off + (metric != kMetricDot ? (size_t)m * 4 : 0));
-  p.off_cn = off;
-  off = al256(off + (metric != kMetricDot ? (size_t)n * 4 : 0));
+  p.off_qn = off;  // [norms m | inverse norms m]
+  off = al256(off + (metric != kMetricDot ? (size_t)m * 8 : 0));
+  p.off_cn = off;  // [norms n | inverse norms n]
+  off = al256(off + (metric != kMetricDot ? (size_t)n * 8 : 0));
   p.total = off;
   (void)d;
   return PMM_OK;
@@ -327,14 +328,16 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     if (metric != kMetricDot) {
       const int sq = metric == kMetricEuclidean;
       Timed t("norms_f32", s);
-      HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, s));
-      HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, s));
+      HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, sq ? nullptr : qn + m, s));
+      HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, sq ? nullptr : cn + n, s));
     }
     GemmF32Args a{};
     a.q = q;
     a.c = c;
     a.qn = qn;
     a.cn = cn;
+    a.qinv = qn + m;
+    a.cinv = cn + n;
     a.ldq = ldq;
     a.ldc = ldc;
     a.M = (int)m;
@@ -389,8 +392,8 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
   float *sc = (float *)(w + p.off_scores);
   if (metric != kMetricDot) {
     const int sq = metric == kMetricEuclidean;
-    HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, s));
-    HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, s));
+    HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
+    HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, nullptr, s));
   }
   for (int64_t r0 = 0; r0 < m; r0 += p.rows) {
     const int64_t rows = std::min<int64_t>(p.rows, m - r0);

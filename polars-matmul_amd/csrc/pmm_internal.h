@@ -24,6 +24,8 @@ struct GemmF32Args {
   const float *c;       // N x ldc
   const float *qn;      // cosine: L2 norms of Q rows; euclidean: squared norms
   const float *cn;      // same for C rows
+  const float *qinv;    // cosine pre-filter: 1/||q|| (0 for a zero-norm row)
+  const float *cinv;    // cosine pre-filter: 1/||c||
   int64_t ldq, ldc;
   int M, N, D;          // D % 32 == 0
   int k, capg;          // top-k and candidate-buffer capacity (power of two)
@@ -65,7 +67,7 @@ struct RowSelArgs {
 
 // ---- launchers (pmm_kernels.hip) ----
 hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld, int squared,
-                            float *out, hipStream_t s);
+                            float *out, float *inv, hipStream_t s);
 hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,
                             double *out, hipStream_t s);
 // Tile-shape variant of the f32 GEMM (see pmm_kernels.hip): 0 = 128x128,

@@ -145,7 +145,7 @@ __device__ __forceinline__ double sqrt_rn<double>(double x) { return __dsqrt_rn(
 template <typename T>
 __global__ __launch_bounds__(256) void norms_kernel(const T *__restrict__ a, int64_t rows,
                                                     int64_t d, int64_t ld, int squared,
-                                                    T *__restrict__ out) {
+                                                    T *__restrict__ out, T *__restrict__ inv) {
   const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t row = gt >> 3;
   const int j = threadIdx.x & 7;
@@ -173,16 +173,19 @@ __global__ __launch_bounds__(256) void norms_kernel(const T *__restrict__ a, int
       const T x = p[i];
       sum = sum + x * x;
     }
-    out[row] = squared ? sum : sqrt_rn<T>(sum);
+    const T v = squared ? sum : sqrt_rn<T>(sum);
+    out[row] = v;
+    // cosine pre-filter factor: 1/norm, 0 for the reference's zero-norm rule
+    if (inv) inv[row] = (v > (T)1e-6) ? (T)1 / v : (T)0;
   }
 }
 
 hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld, int squared,
-                            float *out, hipStream_t s) {
+                            float *out, float *inv, hipStream_t s) {
   if (rows <= 0) return hipSuccess;
   const int64_t threads = rows * 8;
   const unsigned grid = (unsigned)((threads + 255) / 256);
-  norms_kernel<float><<<grid, 256, 0, s>>>(a, rows, d, ld, squared, out);
+  norms_kernel<float><<<grid, 256, 0, s>>>(a, rows, d, ld, squared, out, inv);
   return hipGetLastError();
 }
 hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,
@@ -190,7 +193,7 @@ hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld
   if (rows <= 0) return hipSuccess;
   const int64_t threads = rows * 8;
   const unsigned grid = (unsigned)((threads + 255) / 256);
-  norms_kernel<double><<<grid, 256, 0, s>>>(a, rows, d, ld, squared, out);
+  norms_kernel<double><<<grid, 256, 0, s>>>(a, rows, d, ld, squared, out, nullptr);
   return hipGetLastError();
 }
 
@@ -276,7 +279,10 @@ struct GemmShape {
   static constexpr int BPIECES = B_BYTES / 1024 / NW;  // 1 KiB LDS-DMA pieces per wave
   static constexpr int OFF_THR = 2 * STAGE;
   static constexpr int OFF_CNT = OFF_THR + BM * 8;
-  static constexpr int OFF_UNIT = OFF_CNT + BM * 4;
+  static constexpr int OFF_QEX = OFF_CNT + BM * 4;   // exact row norm (exact path)
+  static constexpr int OFF_RV = OFF_QEX + BM * 4;    // pre-filter row factor
+  static constexpr int OFF_LO = OFF_RV + BM * 4;     // pre-filter bound
+  static constexpr int OFF_UNIT = OFF_LO + BM * 4;
   static constexpr int OFF_SCR = OFF_UNIT + 16;
   static_assert(B_BYTES % (1024 * NW) == 0, "corpus tile must split into 1 KiB pieces per wave");
   static_assert(OFF_SCR % 16 == 0, "LDS carve must stay 16-byte aligned");
@@ -295,7 +301,7 @@ int gemm_f32_bn(int variant) { return 32 * kVarNB[variant]; }
 size_t gemm_f32_lds_bytes(int variant, int mode, int capg) {
   const int nb = kVarNB[variant], nw = kVarNW[variant];
   const size_t stage = (size_t)nw * 4096 + (size_t)32 * nb * 128;
-  const size_t fixed = 2 * stage + (size_t)32 * nw * 12 + 16;
+  const size_t fixed = 2 * stage + (size_t)32 * nw * 24 + 16;
   return fixed + (mode == 0 ? (size_t)nw * capg * 8 : 0);
 }
 
@@ -342,6 +348,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u64 *thr_l = (u64 *)(smem + G::OFF_THR);
   unsigned *cnt_l = (unsigned *)(smem + G::OFF_CNT);
+  float *qex_l = (float *)(smem + G::OFF_QEX);
+  float *rv_l = (float *)(smem + G::OFF_RV);
+  float *lo_l = (float *)(smem + G::OFF_LO);
   int *unit_l = (int *)(smem + G::OFF_UNIT);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -351,6 +360,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   u64 *scr = (u64 *)(smem + G::OFF_SCR) + (size_t)wid * a.capg;
   u64 *thr_w = thr_l + wid * 32;
   unsigned *cnt_w = cnt_l + wid * 32;
+  float *qex_w = qex_l + wid * 32;
+  float *rv_w = rv_l + wid * 32;  // per-row constants live in LDS, not in VGPRs across
+  float *lo_w = lo_l + wid * 32;  // the K loop (keeps the 256x256 tile spill-free)
   constexpr bool XFORM = (METRIC != kMetricDot);
 
   // Loop-invariant per-lane byte offsets of this wave's LDS-DMA pieces.
@@ -388,31 +400,25 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         make_rsrc(a.q + (int64_t)wrow0 * a.ldq, (int64_t)min(32, a.M - wrow0) * a.ldq * 4);
 
     // Per-lane row constants for the 16 accumulator rows this lane holds.
-    float rv[16], lo[16];
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-      const int grow = wrow0 + acc_row(e, h);
+    if (lane < 32) {
+      const int grow = wrow0 + lane;
       float v = 0.0f;
       if (XFORM && grow < a.M) {
-        const float x = a.qn[grow];
-        if (MODE == 0 && METRIC == kMetricCosine) v = (x > 1e-6f) ? 1.0f / x : 0.0f;
-        else v = x;
+        if (MODE == 0 && METRIC == kMetricCosine) v = a.qinv[grow];
+        else v = a.qn[grow];
       }
-      rv[e] = v;
-      lo[e] = 0.0f;
-    }
-    if (MODE == 0) {
-      if (lane < 32) {
-        const int grow = wrow0 + lane;
-        thr_w[lane] = (grow < a.M) ? __hip_atomic_load(a.gthr + grow, __ATOMIC_RELAXED,
+      rv_w[lane] = v;
+      qex_w[lane] = (XFORM && grow < a.M) ? a.qn[grow] : 0.0f;
+      if (MODE == 0) {
+        const u64 t = (grow < a.M) ? __hip_atomic_load(a.gthr + grow, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT)
                                    : ~0ull;
+        thr_w[lane] = t;
+        lo_w[lane] = prefilter_lo<METRIC>(t);
         cnt_w[lane] = 0u;
       }
-      wave_sync();
-#pragma unroll
-      for (int e = 0; e < 16; e++) lo[e] = prefilter_lo<METRIC>(thr_w[acc_row(e, h)]);
     }
+    wave_sync();
 
     auto rsrc_b = [&](int tile) {
       const int col0 = tile * G::BN;
@@ -460,6 +466,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       rb = rbn;
 
       const int col0 = tile * G::BN;
+      float rv[16], lo[16];
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        rv[e] = rv_w[acc_row(e, h)];
+        lo[e] = (MODE == 0) ? lo_w[acc_row(e, h)] : 0.0f;
+      }
       if (MODE == 1) {
         // ---- store epilogue (.pmm.matmul, or materialised scores) ----
 #pragma unroll
@@ -486,13 +498,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           const bool cvalid = gcol < a.N;
           const int gcc = min(gcol, a.N - 1);
           float cv = 0.0f;
-          if (METRIC == kMetricCosine) {
-            const float x = a.cn[gcc];
-            cv = (x > 1e-6f) ? 1.0f / x : 0.0f;
-          } else if (METRIC == kMetricEuclidean) {
-            cv = a.cn[gcc];
-          }
-          bool any = false;
+          if (METRIC == kMetricCosine) cv = a.cinv[gcc];
+          else if (METRIC == kMetricEuclidean) cv = a.cn[gcc];
+          uint32_t pmask = 0u;  // bit e: element e may beat its row's k-th
 #pragma unroll
           for (int e = 0; e < 16; e++) {
             const float v = acc[c][e];
@@ -500,23 +508,24 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             if (METRIC == kMetricDot) pv = v;
             else if (METRIC == kMetricCosine) pv = (v * rv[e]) * cv;
             else pv = fmaf(2.0f, v, -(rv[e] + cv));
-            any |= !(pv < lo[e]);
+            pmask |= (uint32_t)(!(pv < lo[e])) << e;
           }
-          any = any && cvalid;
-          if (__ballot(any) != 0ull) {
-            // exact path: rare after the first tiles of a unit
+          if (!cvalid) pmask = 0u;
+          if (__ballot(pmask != 0u) != 0ull) {
+            // exact path, only for the accumulator rows that have a survivor
             const float cex = XFORM ? a.cn[gcc] : 0.0f;
 #pragma unroll
             for (int e = 0; e < 16; e++) {
-              const int rl = acc_row(e, h);
-              const int grow = wrow0 + rl;
-              const float qex = XFORM ? a.qn[min(grow, a.M - 1)] : 0.0f;
-              const float sc = exact_score<METRIC>(acc[c][e], qex, cex);
-              const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
-              const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
-              if (cvalid && comp > thr_w[rl]) {
-                const unsigned pos = atomicAdd(&cnt_w[rl], 1u);
-                a.cand[((int64_t)grow * a.S + s) * a.capg + pos] = comp;
+              if (__ballot((pmask >> e) & 1u) == 0ull) continue;
+              if ((pmask >> e) & 1u) {
+                const int rl = acc_row(e, h);
+                const float sc = exact_score<METRIC>(acc[c][e], XFORM ? qex_w[rl] : 0.0f, cex);
+                const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
+                const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
+                if (comp > thr_w[rl]) {
+                  const unsigned pos = atomicAdd(&cnt_w[rl], 1u);
+                  a.cand[((int64_t)(wrow0 + rl) * a.S + s) * a.capg + pos] = comp;
+                }
               }
             }
             wave_sync();
@@ -529,8 +538,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
                 need &= need - 1;
                 compact_row(a, s, wrow0 + r, thr_w + r, cnt_w + r, scr, lane);
               }
+              if (lane < 32) lo_w[lane] = prefilter_lo<METRIC>(thr_w[lane]);
+              wave_sync();
 #pragma unroll
-              for (int e = 0; e < 16; e++) lo[e] = prefilter_lo<METRIC>(thr_w[acc_row(e, h)]);
+              for (int e = 0; e < 16; e++) lo[e] = lo_w[acc_row(e, h)];
             }
           }
         }
