@@ -444,8 +444,6 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       for (int c = 0; c < NB; c++) acc[c] = (f32x16){};
       for (int ks = 0; ks < KS; ks++) {
         __syncthreads();  // stage `buf` landed (vmcnt(0) + barrier); buf^1 free
-        if (ks + 1 < KS) stage(buf ^ 1, rb, ks + 1);
-        else if (!last_tile) stage(buf ^ 1, rbn, 0);
         const char *st = smem + buf * G::STAGE;
 #pragma unroll
         for (int qd = 0; qd < 4; qd++) {
@@ -459,6 +457,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
 #pragma unroll
             for (int c = 0; c < NB; c++)
               acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], b[c][j], acc[c], 0, 0, 0);
+          }
+          if (qd == 0) {
+            // next step's LDS-DMA goes out behind the first MFMA group, so the
+            // matrix pipe restarts right after the barrier
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + 1 < KS) stage(buf ^ 1, rb, ks + 1);
+            else if (!last_tile) stage(buf ^ 1, rbn, 0);
+            __builtin_amdgcn_sched_barrier(0);
           }
         }
         buf ^= 1;
