@@ -85,7 +85,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-sample", type=int, default=512, help="queries timed on the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=512,
+                    help="queries timed on the CPU baseline vs the full corpus (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 torch top-k")
     args = ap.parse_args()
@@ -118,33 +119,15 @@ def main():
     q = torch.randn((M, D), generator=g, device=dev, dtype=torch.float32)
     g.manual_seed(1_000_003 + rank)
     c = torch.randn((n_loc, D), generator=g, device=dev, dtype=torch.float32)
-    out_i = torch.empty((M, k), dtype=torch.int32, device=dev)
-    out_s = torch.empty((M, k), dtype=torch.float32, device=dev)
     ws_bytes = _native.workspace_bytes(M, n_loc, D, k, mid)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    if world > 1 and rank == 0:
-        gath_i = [torch.empty((M, k), dtype=torch.int32, device=dev) for _ in range(world)]
-        gath_s = [torch.empty((M, k), dtype=torch.float32, device=dev) for _ in range(world)]
-        fin_i = torch.empty((M, k), dtype=torch.int32, device=dev)
-        fin_s = torch.empty((M, k), dtype=torch.float32, device=dev)
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream().cuda_stream
+    from polars_matmul.sharded import ShardedTopK
 
-    def step():
-        _native.topk_device(q.data_ptr(), D, M, c.data_ptr(), D, n_loc, D, k, mid,
-                            out_i.data_ptr(), out_s.data_ptr(), index_base=lo,
-                            workspace=ws.data_ptr(), workspace_bytes=ws_bytes, stream=stream)
-        if world > 1:
-            dist.gather(out_i, gath_i if rank == 0 else None, dst=0)
-            dist.gather(out_s, gath_s if rank == 0 else None, dst=0)
-            if rank == 0:
-                si = torch.stack(gath_i, dim=1).contiguous()
-                ss = torch.stack(gath_s, dim=1).contiguous()
-                _native.merge_device(si.data_ptr(), ss.data_ptr(), M, world, k, k, mid,
-                                     fin_i.data_ptr(), fin_s.data_ptr(), stream=stream)
+    runner = ShardedTopK(q, c, lo, k, mid, workspace=ws)
+    torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        step()
+        runner.run()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -153,7 +136,7 @@ def main():
     _native.timing_enable(True)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step()
+        out_i, out_s = runner.run()
         log(f"[rank {rank}] step {i + 1}/{args.steps} issued")
     torch.cuda.synchronize()
     if dist:
@@ -163,6 +146,7 @@ def main():
     _native.timing_enable(False)
     kern_ms, kern_n = _native.timing_read("gemm_f32_topk")
     merge_ms, merge_n = _native.timing_read("merge_topk")
+    shard_ms, shard_n = _native.timing_read("merge_shards")
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -203,7 +187,7 @@ def main():
     achieved = flops_launch / avg_kern_s / 1e12 if avg_kern_s else None
     roofline = {
         "bound": "mfma",
-        "kernel": "gemm_f32_kernel<0,cosine> (fused GEMM + top-k)",
+        "kernel": "gemm_f32_kernel (fused GEMM + metric + top-k)",
         "achieved": round(achieved, 2) if achieved else None,
         "peak": F32_MFMA_PEAK_TFLOPS,
         "unit": "TFLOP/s",
@@ -212,6 +196,7 @@ def main():
         "kernel_ms_avg": round(kern_ms / kern_n, 3) if kern_n else None,
         "flops_per_launch": flops_launch,
         "merge_ms_avg": round(merge_ms / merge_n, 3) if merge_n else None,
+        "shard_merge_ms_avg": round(shard_ms / shard_n, 3) if shard_n else None,
     }
     cpu = None
     if args.cpu_sample and world == 1:

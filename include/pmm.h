@@ -114,8 +114,10 @@ size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int 
 /* Fused top-k over device buffers.  ldq / ldc are row strides in elements;
  * d must be a multiple of 32 and ldq/ldc multiples of 4 with 16-byte-aligned
  * bases (pmm_topk_f32 pads host inputs itself).  index_base is added to every
- * returned corpus index (global index of corpus row 0 of this shard).
- * workspace may be NULL (a per-thread cached buffer is used). */
+ * returned corpus index (global index of corpus row 0 of this shard).  For
+ * k <= 1024, k may exceed n (a small shard): slots past n are empty (index
+ * 0xFFFFFFFF, score NaN).  workspace may be NULL (a per-thread cached buffer
+ * is used). */
 int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, int64_t ldc,
                         int64_t n, int64_t d, int64_t k, int metric, int compute,
                         uint32_t index_base, uint32_t *out_idx, float *out_score,

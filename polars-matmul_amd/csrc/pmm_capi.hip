@@ -437,15 +437,16 @@ int upload_padded(void *dst, const void *src, int64_t rows, int64_t d, int64_t d
   return PMM_OK;
 }
 
-int validate_sizes(int64_t m, int64_t n, int64_t d, int64_t k, bool topk) {
+int validate_sizes(int64_t m, int64_t n, int64_t d, int64_t k, bool topk, bool allow_k_gt_n = false) {
   if (m < 0 || n < 0 || d < 0) return fail(PMM_ERR_ARG, "negative size (m=%lld n=%lld d=%lld)",
                                            (long long)m, (long long)n, (long long)d);
   if (m > INT32_MAX || n > (int64_t)UINT32_MAX - 1 || n > INT32_MAX)
     return fail(PMM_ERR_ARG, "size out of range (m=%lld n=%lld)", (long long)m, (long long)n);
   if (topk) {
     if (k < 0) return fail(PMM_ERR_ARG, "k must be >= 0 (got %lld)", (long long)k);
-    if (k > n) return fail(PMM_ERR_ARG, "k (%lld) must be <= n (%lld): clip k to n first",
-                           (long long)k, (long long)n);
+    if (k > n && !allow_k_gt_n)
+      return fail(PMM_ERR_ARG, "k (%lld) must be <= n (%lld): clip k to n first", (long long)k,
+                  (long long)n);
   }
   return PMM_OK;
 }
@@ -515,7 +516,9 @@ int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, 
                         int64_t n, int64_t d, int64_t k, int metric, int compute,
                         uint32_t index_base, uint32_t *out_idx, float *out_score, void *workspace,
                         size_t workspace_bytes, void *stream) {
-  int rc = validate_sizes(m, n, d, k, true);
+  // a corpus shard may hold fewer than k rows: the fused path pads with empty
+  // slots (index 0xFFFFFFFF, score NaN), which the shard merge skips
+  int rc = validate_sizes(m, n, d, k, true, k <= kFusedMaxK);
   if (rc) return rc;
   if ((rc = check_metric(metric))) return rc;
   if (compute != PMM_COMPUTE_F32)
