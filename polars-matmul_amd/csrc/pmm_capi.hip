@@ -169,6 +169,7 @@ struct Plan {
   int variant = 0;
   int QB = 0, T = 0, tps = 0, S = 0, units = 0, grid = 0, capg = 0, P = 0;
   size_t off_counter = 0, off_gthr = 0, off_cnt = 0, off_cand = 0, off_qn = 0, off_cn = 0;
+  size_t off_wq = 0;
   size_t total = 0;
 };
 
@@ -234,6 +235,9 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   off = al256(off + (metric != kMetricDot ? (size_t)m * 8 : 0));
   p.off_cn = off;  // [norms n | inverse norms n]
   off = al256(off + (metric != kMetricDot ? (size_t)n * 8 : 0));
+  p.off_wq = off;  // per-wave survivor queues: grid x waves x (32 x BN) u64
+  off = al256(off + (size_t)p.grid * (gemm_f32_bm(p.variant) / 32) * 32 *
+                        gemm_f32_bn(p.variant) * 8);
   p.total = off;
   (void)d;
   return PMM_OK;
@@ -328,16 +332,15 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     if (metric != kMetricDot) {
       const int sq = metric == kMetricEuclidean;
       Timed t("norms_f32", s);
-      HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, sq ? nullptr : qn + m, s));
-      HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, sq ? nullptr : cn + n, s));
+      HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
+      HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, cn + n, s));
     }
     GemmF32Args a{};
     a.q = q;
     a.c = c;
     a.qn = qn;
     a.cn = cn;
-    a.qinv = qn + m;
-    a.cinv = cn + n;
+    a.cpre = cn + n;
     a.ldq = ldq;
     a.ldc = ldc;
     a.M = (int)m;
@@ -352,7 +355,12 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     a.ntiles = p.T;
     a.units = p.units;
     a.counter = (unsigned *)(w + p.off_counter);
+    {
+      static const int ablate = getenv("PMM_ABLATE") ? atoi(getenv("PMM_ABLATE")) : 0;
+      a.ablate = ablate;
+    }
     a.cand = (unsigned long long *)(w + p.off_cand);
+    a.wq = (unsigned long long *)(w + p.off_wq);
     a.cnt = (unsigned *)(w + p.off_cnt);
     a.gthr = (unsigned long long *)(w + p.off_gthr);
     {

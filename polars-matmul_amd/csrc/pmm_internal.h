@@ -24,8 +24,8 @@ struct GemmF32Args {
   const float *c;       // N x ldc
   const float *qn;      // cosine: L2 norms of Q rows; euclidean: squared norms
   const float *cn;      // same for C rows
-  const float *qinv;    // cosine pre-filter: 1/||q|| (0 for a zero-norm row)
-  const float *cinv;    // cosine pre-filter: 1/||c||
+  const float *cpre;    // pre-filter column factor: cosine 1/||c|| (0 if zero-norm),
+                        // euclidean ||c||^2 * (1 - 2^-18)
   int64_t ldq, ldc;
   int M, N, D;          // D % 32 == 0
   int k, capg;          // top-k and candidate-buffer capacity (power of two)
@@ -35,9 +35,11 @@ struct GemmF32Args {
   unsigned long long *cand;       // [M*S][capg] candidate composites
   unsigned *cnt;                  // [M*S] candidate counts
   unsigned long long *gthr;       // [M] shared per-row threshold, zeroed per call
+  unsigned long long *wq;         // per-wave survivor queue [grid][NW][32 * BN]
   float *out;                     // store mode: out[M][ldo]
   int64_t ldo;
   int store_metric;               // store mode: 1 = metric-transformed score, 0 = raw dot
+  int ablate;                     // benchmarking only (PMM_ABLATE): 1 = skip the epilogue
 };
 
 struct MergeArgs {

@@ -175,8 +175,10 @@ __global__ __launch_bounds__(256) void norms_kernel(const T *__restrict__ a, int
     }
     const T v = squared ? sum : sqrt_rn<T>(sum);
     out[row] = v;
-    // cosine pre-filter factor: 1/norm, 0 for the reference's zero-norm rule
-    if (inv) inv[row] = (v > (T)1e-6) ? (T)1 / v : (T)0;
+    // pre-filter column factor (see prefilter_bound): cosine 1/norm (0 for the
+    // reference's zero-norm rule); euclidean the squared norm shrunk by 2^-18
+    // so 2*dot - factor over-estimates qsq - sq by more than its rounding.
+    if (inv) inv[row] = squared ? v * (T)(1.0 - 0x1p-18) : ((v > (T)1e-6) ? (T)1 / v : (T)0);
   }
 }
 
@@ -226,25 +228,33 @@ __device__ __forceinline__ double exact_score_f64(double dot, double qv, double 
   return __dsqrt_rn(mx);
 }
 
-// Pre-filter bound.  The pre-filter value pv of a score is
-//   dot:    pv = dot                       (exact)
-//   cosine: pv = (dot * (1/qn)) * (1/cn)   (<= 6 ulp from the exact score)
-//   euclid: pv = 2*dot - (qsq + csq)       (= -sq exactly)
-// and an element can only beat the row's current k-th composite `thr` if
-// !(pv < lo).  lo is loose by a margin that covers the approximation, so
-// the pre-filter never rejects a true candidate; survivors are re-tested
-// exactly against the composite.
+// Pre-filter.  For every score the hot epilogue computes ONE value
+//   dot:    pv = dot                     (exact)
+//   cosine: pv = dot * (1/cn)            (= score * qn within 5 ulp)
+//   euclid: pv = 2*dot - csq*(1-2^-18)   (>= qsq - sq - rounding)
+// and keeps the element iff !(pv < L), with the per-row bound L derived from
+// the row's current k-th composite `thr` and the row norm qv (cosine: ||q||,
+// euclid: ||q||^2).  L is loose by a margin that covers every rounding step,
+// so the pre-filter never rejects a true candidate; survivors are re-scored
+// exactly and compared as composites.  NaN pv always passes (!(NaN < L)).
 template <int METRIC>
-__device__ __forceinline__ float prefilter_lo(u64 thr) {
-  if (thr == ~0ull) return __builtin_inff();             // padding row: reject all
+__device__ __forceinline__ float prefilter_bound(u64 thr, float qv) {
+  const float inf = __builtin_inff();
+  if (thr == ~0ull) return inf;                 // padding row: reject all
   const uint32_t tk = (uint32_t)(thr >> 32);
-  if (tk == 0u) return -__builtin_inff();                 // row not full: accept all
-  const float v = dekey32(tk);                            // ranking value of the k-th
+  if (tk == 0u) return -inf;                    // row not full: accept all
+  const float v = dekey32(tk);                  // ranking value of the k-th
   if (METRIC == kMetricDot) return v;
-  if (METRIC == kMetricCosine) return v - (fabsf(v) * 0x1p-20f + 0x1p-100f);
+  if (METRIC == kMetricCosine) {
+    if (!(qv > 1e-6f)) return (0.0f >= v) ? -inf : inf;  // zero-norm row: every score is 0
+    const float lo = v - (fabsf(v) * 0x1p-19f + 0x1p-100f);
+    const float L = lo * qv;
+    return L - (fabsf(L) * 0x1p-20f + 0x1p-100f);
+  }
   const float dist = -v;
   const float hi = dist * dist * (1.0f + 0x1p-20f) + 0x1p-100f;
-  return -hi;
+  const float L = qv - hi;
+  return L - ((fabsf(qv) + hi) * 0x1p-18f + 0x1p-100f);
 }
 
 // ===========================================================================
@@ -279,10 +289,10 @@ struct GemmShape {
   static constexpr int BPIECES = B_BYTES / 1024 / NW;  // 1 KiB LDS-DMA pieces per wave
   static constexpr int OFF_THR = 2 * STAGE;
   static constexpr int OFF_CNT = OFF_THR + BM * 8;
-  static constexpr int OFF_QEX = OFF_CNT + BM * 4;   // exact row norm (exact path)
-  static constexpr int OFF_RV = OFF_QEX + BM * 4;    // pre-filter row factor
-  static constexpr int OFF_LO = OFF_RV + BM * 4;     // pre-filter bound
-  static constexpr int OFF_UNIT = OFF_LO + BM * 4;
+  static constexpr int OFF_QEX = OFF_CNT + BM * 4;   // exact row norm (epilogue)
+  static constexpr int OFF_LO = OFF_QEX + BM * 4;    // pre-filter bound per row
+  static constexpr int OFF_CV = OFF_LO + BM * 4;     // column factors, 2 tiles
+  static constexpr int OFF_UNIT = OFF_CV + 2 * BN * 4;
   static constexpr int OFF_SCR = OFF_UNIT + 16;
   static_assert(B_BYTES % (1024 * NW) == 0, "corpus tile must split into 1 KiB pieces per wave");
   static_assert(OFF_SCR % 16 == 0, "LDS carve must stay 16-byte aligned");
@@ -301,7 +311,7 @@ int gemm_f32_bn(int variant) { return 32 * kVarNB[variant]; }
 size_t gemm_f32_lds_bytes(int variant, int mode, int capg) {
   const int nb = kVarNB[variant], nw = kVarNW[variant];
   const size_t stage = (size_t)nw * 4096 + (size_t)32 * nb * 128;
-  const size_t fixed = 2 * stage + (size_t)32 * nw * 24 + 16;
+  const size_t fixed = 2 * stage + (size_t)32 * nw * 20 + (size_t)2 * 32 * nb * 4 + 16;
   return fixed + (mode == 0 ? (size_t)nw * capg * 8 : 0);
 }
 
@@ -349,8 +359,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   u64 *thr_l = (u64 *)(smem + G::OFF_THR);
   unsigned *cnt_l = (unsigned *)(smem + G::OFF_CNT);
   float *qex_l = (float *)(smem + G::OFF_QEX);
-  float *rv_l = (float *)(smem + G::OFF_RV);
   float *lo_l = (float *)(smem + G::OFF_LO);
+  float *cv_l = (float *)(smem + G::OFF_CV);
   int *unit_l = (int *)(smem + G::OFF_UNIT);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -360,9 +370,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   u64 *scr = (u64 *)(smem + G::OFF_SCR) + (size_t)wid * a.capg;
   u64 *thr_w = thr_l + wid * 32;
   unsigned *cnt_w = cnt_l + wid * 32;
-  float *qex_w = qex_l + wid * 32;
-  float *rv_w = rv_l + wid * 32;  // per-row constants live in LDS, not in VGPRs across
-  float *lo_w = lo_l + wid * 32;  // the K loop (keeps the 256x256 tile spill-free)
+  float *qex_w = qex_l + wid * 32;  // per-row constants live in LDS, not in VGPRs
+  float *lo_w = lo_l + wid * 32;    // across the K loop (keeps 256x256 spill-free)
   constexpr bool XFORM = (METRIC != kMetricDot);
 
   // Loop-invariant per-lane byte offsets of this wave's LDS-DMA pieces.
@@ -402,19 +411,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     // Per-lane row constants for the 16 accumulator rows this lane holds.
     if (lane < 32) {
       const int grow = wrow0 + lane;
-      float v = 0.0f;
-      if (XFORM && grow < a.M) {
-        if (MODE == 0 && METRIC == kMetricCosine) v = a.qinv[grow];
-        else v = a.qn[grow];
-      }
-      rv_w[lane] = v;
-      qex_w[lane] = (XFORM && grow < a.M) ? a.qn[grow] : 0.0f;
+      const float qv = (XFORM && grow < a.M) ? a.qn[grow] : 0.0f;
+      qex_w[lane] = qv;
       if (MODE == 0) {
         const u64 t = (grow < a.M) ? __hip_atomic_load(a.gthr + grow, __ATOMIC_RELAXED,
                                                         __HIP_MEMORY_SCOPE_AGENT)
                                    : ~0ull;
         thr_w[lane] = t;
-        lo_w[lane] = prefilter_lo<METRIC>(t);
+        lo_w[lane] = prefilter_bound<METRIC>(t, qv);
         cnt_w[lane] = 0u;
       }
     }
@@ -424,7 +428,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       const int col0 = tile * G::BN;
       return make_rsrc(a.c + (int64_t)col0 * a.ldc, (int64_t)min(G::BN, a.N - col0) * a.ldc * 4);
     };
-    auto stage = [&](int sb, __amdgpu_buffer_rsrc_t rb, int ks) {
+    auto stage = [&](int sb, __amdgpu_buffer_rsrc_t rb, int ks, int tile) {
       char *st = smem + sb * G::STAGE;
       const uint32_t soff = (uint32_t)ks * 128u;
 #pragma unroll
@@ -432,10 +436,21 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
 #pragma unroll
       for (int i = 0; i < G::BPIECES; i++)
         dma16(rb, st + G::A_BYTES + (i * NW + wid) * 1024, b_voff[i], soff);
+      if (MODE == 0 && XFORM && ks == 0 && wid == 0) {
+        // the tile's pre-filter column factors ride with its first K step
+        const int col0 = tile * G::BN;
+        const __amdgpu_buffer_rsrc_t rc =
+            make_rsrc(a.cpre + col0, (int64_t)min(G::BN, a.N - col0) * 4);
+        char *dst = (char *)(cv_l + (tile & 1) * G::BN);
+#pragma unroll
+        for (int i = 0; i < G::BN / 64; i++)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (LDS_AS void *)(dst + i * 256), 4,
+                                                   (uint32_t)(lane * 4 + i * 256), 0, 0, 0);
+      }
     };
 
     __amdgpu_buffer_rsrc_t rb = rsrc_b(t0);
-    stage(buf, rb, 0);
+    stage(buf, rb, 0, t0);
     for (int tile = t0; tile < t1; tile++) {
       const bool last_tile = (tile + 1) >= t1;
       const __amdgpu_buffer_rsrc_t rbn = last_tile ? rb : rsrc_b(tile + 1);
@@ -462,8 +477,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             // next step's LDS-DMA goes out behind the first MFMA group, so the
             // matrix pipe restarts right after the barrier
             __builtin_amdgcn_sched_barrier(0);
-            if (ks + 1 < KS) stage(buf ^ 1, rb, ks + 1);
-            else if (!last_tile) stage(buf ^ 1, rbn, 0);
+            if (ks + 1 < KS) stage(buf ^ 1, rb, ks + 1, tile);
+            else if (!last_tile) stage(buf ^ 1, rbn, 0, tile + 1);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -472,10 +487,20 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       rb = rbn;
 
       const int col0 = tile * G::BN;
+      if (a.ablate == 1) {
+        // ablation build path: keep the accumulators live, skip the epilogue
+        float sink = 0.0f;
+#pragma unroll
+        for (int c = 0; c < NB; c++)
+#pragma unroll
+          for (int e = 0; e < 16; e++) sink += acc[c][e];
+        asm volatile("" ::"v"(sink));
+        continue;
+      }
       float rv[16], lo[16];
 #pragma unroll
       for (int e = 0; e < 16; e++) {
-        rv[e] = rv_w[acc_row(e, h)];
+        rv[e] = qex_w[acc_row(e, h)];
         lo[e] = (MODE == 0) ? lo_w[acc_row(e, h)] : 0.0f;
       }
       if (MODE == 1) {
@@ -498,45 +523,68 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         }
       } else {
         // ---- fused top-k epilogue ----
+        // Pass 1 (accumulators live): one pre-filter op + compare per score;
+        // survivors (rare after a unit's first tiles) are appended to this
+        // wave's queue with ballot + mbcnt slots (no atomics).  Pass 2
+        // (accumulators dead): re-score the queue exactly, 64 items at a time
+        // (one per lane), and append to the rows' candidate buffers.  The
+        // queue lives in global memory (L2): a tile can produce up to
+        // 32 x BN survivors per wave (a unit's first tile).
+        const float *cvt = cv_l + (tile & 1) * G::BN;
+        u64 *gq = a.wq + ((size_t)blockIdx.x * NW + wid) * (size_t)(32 * G::BN);
+        int qlen = 0;  // wave-uniform
+        // queue item high word = row-in-wave | col-in-tile << 5 = lane part +
+        // a per-(c, e) constant; the opaque zero keeps the compiler from
+        // hoisting all 16*NB constants out of the tile loop into registers
+        uint32_t opaque0;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(opaque0));
+        const uint32_t lane_hi = opaque0 + 4u * (uint32_t)h + ((uint32_t)r32 << 5);
 #pragma unroll
         for (int c = 0; c < NB; c++) {
           const int gcol = col0 + 32 * c + r32;
           const bool cvalid = gcol < a.N;
-          const int gcc = min(gcol, a.N - 1);
-          float cv = 0.0f;
-          if (METRIC == kMetricCosine) cv = a.cinv[gcc];
-          else if (METRIC == kMetricEuclidean) cv = a.cn[gcc];
-          uint32_t pmask = 0u;  // bit e: element e may beat its row's k-th
+          const float cv = XFORM ? cvt[32 * c + r32] : 0.0f;
 #pragma unroll
           for (int e = 0; e < 16; e++) {
             const float v = acc[c][e];
             float pv;
             if (METRIC == kMetricDot) pv = v;
-            else if (METRIC == kMetricCosine) pv = (v * rv[e]) * cv;
-            else pv = fmaf(2.0f, v, -(rv[e] + cv));
-            pmask |= (uint32_t)(!(pv < lo[e])) << e;
+            else if (METRIC == kMetricCosine) pv = v * cv;
+            else pv = fmaf(2.0f, v, -cv);
+            const bool p = cvalid && !(pv < lo[e]);
+            const u64 m = __ballot(p);
+            if (m == 0ull) continue;
+            if (p && a.ablate != 2) {
+              const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
+              gq[qlen + lanes_below(m)] = (u64)__float_as_uint(v) | ((u64)hi << 32);
+            }
+            qlen += __popcll(m);
           }
-          if (!cvalid) pmask = 0u;
-          if (__ballot(pmask != 0u) != 0ull) {
-            // exact path, only for the accumulator rows that have a survivor
-            const float cex = XFORM ? a.cn[gcc] : 0.0f;
-#pragma unroll
-            for (int e = 0; e < 16; e++) {
-              if (__ballot((pmask >> e) & 1u) == 0ull) continue;
-              if ((pmask >> e) & 1u) {
-                const int rl = acc_row(e, h);
-                const float sc = exact_score<METRIC>(acc[c][e], XFORM ? qex_w[rl] : 0.0f, cex);
-                const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
-                const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
-                if (comp > thr_w[rl]) {
-                  const unsigned pos = atomicAdd(&cnt_w[rl], 1u);
-                  a.cand[((int64_t)(wrow0 + rl) * a.S + s) * a.capg + pos] = comp;
-                }
+        }
+        if (a.ablate == 2) qlen = 0;  // ablation: pre-filter only
+        if (qlen) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // queue stores reached L2
+          for (int base = 0; base < qlen; base += 64) {
+            const int i = base + lane;
+            if (i < qlen) {
+              // sc1 load: bypasses this CU's L1, reads what the stores left in L2
+              const u64 it = __hip_atomic_load(gq + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const float v = __uint_as_float((uint32_t)it);
+              const int rl = (int)((it >> 32) & 31u);
+              const int gcol = col0 + (int)(it >> 37);
+              const float sc =
+                  exact_score<METRIC>(v, XFORM ? qex_w[rl] : 0.0f, XFORM ? a.cn[gcol] : 0.0f);
+              const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
+              const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
+              if (comp > thr_w[rl]) {
+                const unsigned pos = atomicAdd(&cnt_w[rl], 1u);
+                a.cand[((int64_t)(wrow0 + rl) * a.S + s) * a.capg + pos] = comp;
               }
             }
+            // compact every row whose buffer could overflow on the next 64 appends
             wave_sync();
             const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
-            u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 32));
+            u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 64));
             if (need) {
               asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
               while (need) {
@@ -544,10 +592,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
                 need &= need - 1;
                 compact_row(a, s, wrow0 + r, thr_w + r, cnt_w + r, scr, lane);
               }
-              if (lane < 32) lo_w[lane] = prefilter_lo<METRIC>(thr_w[lane]);
+              if (lane < 32) lo_w[lane] = prefilter_bound<METRIC>(thr_w[lane], qex_w[lane]);
               wave_sync();
-#pragma unroll
-              for (int e = 0; e < 16; e++) lo[e] = lo_w[acc_row(e, h)];
             }
           }
         }
