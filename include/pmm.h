@@ -111,9 +111,11 @@ int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64
 size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int metric,
                                 int compute);
 
-/* Fused top-k over device buffers.  ldq / ldc are row strides in elements;
- * d must be a multiple of 32 and ldq/ldc multiples of 4 with 16-byte-aligned
- * bases (pmm_topk_f32 pads host inputs itself).  index_base is added to every
+/* Fused top-k over device buffers.  d is the logical dimension; ldq / ldc are
+ * row strides in elements, multiples of 4 and >= roundup(d, 32), with columns
+ * d..roundup(d, 32)-1 zero-filled and 16-byte-aligned bases (pmm_topk_f32 pads
+ * host inputs itself).  Norms use exactly d elements in the reference's order
+ * (ndarray unrolled_dot).  index_base is added to every
  * returned corpus index (global index of corpus row 0 of this shard).  For
  * k <= 1024, k may exceed n (a small shard): slots past n are empty (index
  * 0xFFFFFFFF, score NaN).  workspace may be NULL (a per-thread cached buffer
@@ -132,6 +134,25 @@ int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, 
 int pmm_merge_topk_device(const uint32_t *idx, const float *score, int64_t m, int64_t lists,
                           int64_t k_in, int64_t k_out, int metric, uint32_t *out_idx,
                           float *out_score, void *stream);
+
+/* ---------------------------------------------------------------------------
+ * Device-resident corpus: upload a corpus once and run many top-k calls
+ * against it (Polars' map_batches may call `_topk` repeatedly with the same
+ * corpus Series: python/polars_matmul/__init__.py:115-119).  The handle keeps
+ * the padded rows in HBM and the norms of every metric (src/metrics.rs:368-393,
+ * computed once at creation).  A handle may be used from several threads
+ * concurrently; it is bound to the device current at creation.
+ * ------------------------------------------------------------------------- */
+typedef struct pmm_corpus pmm_corpus;
+
+int pmm_corpus_create_f32(const float *c, int64_t n, int64_t d, pmm_corpus **out);
+int pmm_corpus_destroy(pmm_corpus *corpus);
+int pmm_corpus_info(const pmm_corpus *corpus, int64_t *n, int64_t *d, int *device);
+
+/* pmm_topk_f32 against a device-resident corpus (host queries in, host
+ * results out; 0 <= k <= n). */
+int pmm_topk_f32_corpus(const pmm_corpus *corpus, const float *q, int64_t m, int64_t k,
+                        int metric, uint32_t *out_idx, float *out_score);
 
 /* Per-kernel timing on the launch stream (hipEvents around each launch).
  * enable=1 starts recording; pmm_timing_read returns the summed milliseconds

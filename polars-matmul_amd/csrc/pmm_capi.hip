@@ -312,14 +312,21 @@ int gemm_store_f32(const float *q, int64_t ldq, int64_t rows, const float *c, in
   return PMM_OK;
 }
 
+// c_norms: optional precomputed corpus norms for `metric` laid out as
+// [n norms | n pre-filter factors] (a pmm_corpus handle's cache); NULL =
+// compute them in this call.
 int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c, int64_t ldc,
                          int64_t n, int64_t d, int64_t k, int metric, uint32_t index_base,
                          uint32_t *out_idx, float *out_score, void *ws, size_t ws_bytes,
-                         hipStream_t s, int dev) {
+                         hipStream_t s, int dev, const float *c_norms = nullptr) {
+  // d is the logical dimension (norms follow ndarray's order over exactly d
+  // elements); the GEMM runs over dp = roundup(d, 32), the rows being
+  // zero-padded up to dp.
   const int cus = g_dev[dev].cus;
+  const int64_t dp = cdiv(d, 32) * 32;
   if (k <= kFusedMaxK) {
     Plan p;
-    plan_topk(m, n, d, k, metric, cus, p);
+    plan_topk(m, n, dp, k, metric, cus, p);
     if (!ws) {
       int rc = arena(dev, s, p.total, &ws);
       if (rc) return rc;
@@ -328,12 +335,13 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     }
     char *w = (char *)ws;
     float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
+    if (c_norms) cn = const_cast<float *>(c_norms);
     HIP_TRY(hipMemsetAsync(w, 0, p.off_gthr + (size_t)m * 8, s));
     if (metric != kMetricDot) {
       const int sq = metric == kMetricEuclidean;
       Timed t("norms_f32", s);
       HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
-      HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, cn + n, s));
+      if (!c_norms) HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, cn + n, s));
     }
     GemmF32Args a{};
     a.q = q;
@@ -345,7 +353,7 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     a.ldc = ldc;
     a.M = (int)m;
     a.N = (int)n;
-    a.D = (int)d;
+    a.D = (int)dp;
     a.k = (int)k;
     a.capg = p.capg;
     a.metric = metric;
@@ -398,14 +406,15 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
   char *w = (char *)ws;
   float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
   float *sc = (float *)(w + p.off_scores);
+  if (c_norms) cn = const_cast<float *>(c_norms);
   if (metric != kMetricDot) {
     const int sq = metric == kMetricEuclidean;
     HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
-    HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, nullptr, s));
+    if (!c_norms) HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, nullptr, s));
   }
   for (int64_t r0 = 0; r0 < m; r0 += p.rows) {
     const int64_t rows = std::min<int64_t>(p.rows, m - r0);
-    int rc = gemm_store_f32(q + r0 * ldq, ldq, rows, c, ldc, n, d, metric, 1, qn + r0, cn, sc, n,
+    int rc = gemm_store_f32(q + r0 * ldq, ldq, rows, c, ldc, n, dp, metric, 1, qn + r0, cn, sc, n,
                             (unsigned *)(w + p.off_counter), cus, s);
     if (rc) return rc;
     if (!p.global_sort) {
@@ -460,6 +469,15 @@ int validate_sizes(int64_t m, int64_t n, int64_t d, int64_t k, bool topk, bool a
 }
 
 }  // namespace
+
+// Device-resident corpus (pmm_corpus_*): padded f32 rows in HBM plus the
+// norms / pre-filter factors of every metric, computed once at creation.
+struct pmm_corpus {
+  int device = 0;
+  int64_t n = 0, d = 0, dp = 0;
+  float *data = nullptr;    // n x dp
+  float *norms = nullptr;   // [cosine: n norms | n 1/norm][euclid: n sq | n sq*(1-2^-18)]
+};
 
 // ===========================================================================
 // C ABI
@@ -533,10 +551,12 @@ int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, 
     return fail(PMM_ERR_UNSUPPORTED, "compute mode %d not available in this build", compute);
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
-  if (d % 32 != 0 || ldq % 4 != 0 || ldc % 4 != 0 || ldq < d || ldc < d ||
-      ((uintptr_t)q & 15) || ((uintptr_t)c & 15))
+  const int64_t dp = cdiv(d, 32) * 32;
+  if (d == 0 || ldq % 4 != 0 || ldc % 4 != 0 || ldq < dp || ldc < dp || ((uintptr_t)q & 15) ||
+      ((uintptr_t)c & 15))
     return fail(PMM_ERR_ARG,
-                "device inputs need d %% 32 == 0, 16-byte-aligned rows (d=%lld ldq=%lld ldc=%lld)",
+                "device inputs need row strides >= roundup(d, 32) (zero-padded), multiples of 4, "
+                "16-byte-aligned bases (d=%lld ldq=%lld ldc=%lld)",
                 (long long)d, (long long)ldq, (long long)ldc);
   int dev;
   if ((rc = ensure_device(&dev))) return rc;
@@ -569,7 +589,7 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
   if ((rc = upload_padded(b + off_q, q, m, d, dp, 4, s))) return rc;
   if ((rc = upload_padded(b + off_c, c, n, d, dp, 4, s))) return rc;
   rc = topk_f32_device_impl((const float *)(b + off_q), dp, m, (const float *)(b + off_c), dp, n,
-                            dp, k, metric, 0u, (uint32_t *)(b + off_i), (float *)(b + off_s),
+                            d, k, metric, 0u, (uint32_t *)(b + off_i), (float *)(b + off_s),
                             b + off_w, ws_need, s, dev);
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
@@ -738,6 +758,97 @@ int pmm_merge_topk_device(const uint32_t *idx, const float *score, int64_t m, in
   ma.out_score = out_score;
   Timed t("merge_shards", s);
   HIP_TRY(launch_merge(ma, 1, s));
+  return PMM_OK;
+}
+
+int pmm_corpus_create_f32(const float *c, int64_t n, int64_t d, pmm_corpus **out) {
+  if (!out) return fail(PMM_ERR_ARG, "null argument");
+  *out = nullptr;
+  int rc = validate_sizes(0, n, d, 0, false);
+  if (rc) return rc;
+  if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
+  if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s;
+  if ((rc = thread_stream(dev, &s))) return rc;
+  pmm_corpus *h = new pmm_corpus();
+  h->device = dev;
+  h->n = n;
+  h->d = d;
+  h->dp = cdiv(d, 32) * 32;
+  hipError_t e = hipMalloc(&h->data, (size_t)n * h->dp * 4);
+  if (e == hipSuccess) e = hipMalloc(&h->norms, (size_t)n * 4 * 4);
+  if (e != hipSuccess) {
+    if (h->data) (void)hipFree(h->data);
+    delete h;
+    return fail(PMM_ERR_HIP, "corpus allocation failed: %s", hipGetErrorString(e));
+  }
+  if ((rc = upload_padded(h->data, c, n, d, h->dp, 4, s))) {
+    pmm_corpus_destroy(h);
+    return rc;
+  }
+  hipError_t e1 = launch_norms_f32(h->data, n, d, h->dp, 0, h->norms, h->norms + n, s);
+  hipError_t e2 = launch_norms_f32(h->data, n, d, h->dp, 1, h->norms + 2 * n, h->norms + 3 * n, s);
+  hipError_t e3 = hipStreamSynchronize(s);
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+    pmm_corpus_destroy(h);
+    return fail(PMM_ERR_HIP, "corpus norms failed");
+  }
+  *out = h;
+  return PMM_OK;
+}
+
+int pmm_corpus_destroy(pmm_corpus *h) {
+  if (!h) return PMM_OK;
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  (void)hipSetDevice(h->device);
+  (void)hipDeviceSynchronize();
+  if (h->data) (void)hipFree(h->data);
+  if (h->norms) (void)hipFree(h->norms);
+  (void)hipSetDevice(cur);
+  delete h;
+  return PMM_OK;
+}
+
+int pmm_corpus_info(const pmm_corpus *h, int64_t *n, int64_t *d, int *device) {
+  if (!h) return fail(PMM_ERR_ARG, "null corpus");
+  if (n) *n = h->n;
+  if (d) *d = h->d;
+  if (device) *device = h->device;
+  return PMM_OK;
+}
+
+int pmm_topk_f32_corpus(const pmm_corpus *h, const float *q, int64_t m, int64_t k, int metric,
+                        uint32_t *out_idx, float *out_score) {
+  if (!h) return fail(PMM_ERR_ARG, "null corpus");
+  int rc = validate_sizes(m, h->n, h->d, k, true);
+  if (rc) return rc;
+  if ((rc = check_metric(metric))) return rc;
+  if (m == 0 || k == 0) return PMM_OK;
+  t_ctx.device = h->device;
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s;
+  if ((rc = thread_stream(dev, &s))) return rc;
+  const int64_t dp = h->dp;
+  size_t ws_need = pmm_topk_workspace_bytes(m, h->n, dp, k, metric, PMM_COMPUTE_F32);
+  size_t off_q = 0, off_i = al256((size_t)m * dp * 4);
+  size_t off_s = off_i + al256((size_t)m * k * 4), off_w = off_s + al256((size_t)m * k * 4);
+  void *base;
+  if ((rc = arena(dev, s, off_w + ws_need, &base))) return rc;
+  char *b = (char *)base;
+  if ((rc = upload_padded(b + off_q, q, m, h->d, dp, 4, s))) return rc;
+  const float *cn = metric == kMetricCosine ? h->norms
+                    : metric == kMetricEuclidean ? h->norms + 2 * h->n : nullptr;
+  rc = topk_f32_device_impl((const float *)(b + off_q), dp, m, h->data, dp, h->n, h->d, k, metric,
+                            0u, (uint32_t *)(b + off_i), (float *)(b + off_s), b + off_w, ws_need,
+                            s, dev, cn);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
   return PMM_OK;
 }
 

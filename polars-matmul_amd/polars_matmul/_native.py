@@ -46,6 +46,10 @@ EXPORTED_SYMBOLS = (
     "pmm_topk_workspace_bytes",
     "pmm_topk_f32_device",
     "pmm_merge_topk_device",
+    "pmm_corpus_create_f32",
+    "pmm_corpus_destroy",
+    "pmm_corpus_info",
+    "pmm_topk_f32_corpus",
     "pmm_timing_enable",
     "pmm_timing_reset",
     "pmm_timing_read",
@@ -91,6 +95,13 @@ _SIGS = {
         _i32,
     ),
     "pmm_merge_topk_device": ([_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp], _i32),
+    "pmm_corpus_create_f32": ([_vp, _i64, _i64, ctypes.POINTER(ctypes.c_void_p)], _i32),
+    "pmm_corpus_destroy": ([_vp], _i32),
+    "pmm_corpus_info": (
+        [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)],
+        _i32,
+    ),
+    "pmm_topk_f32_corpus": ([_vp, _vp, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_timing_enable": ([_i32], _i32),
     "pmm_timing_reset": ([], _i32),
     "pmm_timing_read": (
@@ -202,3 +213,36 @@ def timing_read(kernel: str):
     n = ctypes.c_int64(0)
     check(_lib.pmm_timing_read(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)))
     return ms.value, n.value
+
+
+class DeviceCorpus:
+    """An f32 corpus uploaded once to HBM with its norms (pmm_corpus_*)."""
+
+    def __init__(self, c: np.ndarray):
+        c = np.ascontiguousarray(c, dtype=np.float32)
+        h = ctypes.c_void_p()
+        check(_lib.pmm_corpus_create_f32(ptr(c), c.shape[0], c.shape[1], ctypes.byref(h)))
+        self._h = h
+        self.n, self.d = c.shape
+        self.nbytes = c.nbytes
+
+    def topk(self, q: np.ndarray, k: int, metric: int):
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        if q.shape[1] != self.d:
+            raise ValueError("dimension mismatch")
+        m = q.shape[0]
+        idx = np.empty((m, k), dtype=np.uint32)
+        sc = np.empty((m, k), dtype=np.float32)
+        check(_lib.pmm_topk_f32_corpus(self._h, ptr(q), m, k, metric, ptr(idx), ptr(sc)))
+        return idx, sc
+
+    def close(self) -> None:
+        if self._h:
+            _lib.pmm_corpus_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -26,6 +26,10 @@ src/matmul.rs:276-283).
 """
 from __future__ import annotations
 
+import collections
+import os
+import threading
+
 import numpy as np
 import pyarrow as pa
 import pyarrow.compute as pc
@@ -171,6 +175,55 @@ def _as_usize(k) -> int:
 
 
 # ---------------------------------------------------------------------------
+# Device-resident corpus cache.  Polars' map_batches may
+# call _topk repeatedly with the same corpus Series; Arrow buffers are
+# immutable, so an Arrow corpus is identified by its buffers' addresses and
+# sizes while the cache holds a reference to it (the addresses cannot be
+# reused meanwhile).  numpy inputs are mutable and are never cached.
+# PMM_CORPUS_CACHE=0 disables; PMM_CORPUS_CACHE_BYTES bounds HBM use.
+# ---------------------------------------------------------------------------
+
+_cache_lock = threading.Lock()
+_cache: "collections.OrderedDict" = collections.OrderedDict()
+_CACHE_ON = os.environ.get("PMM_CORPUS_CACHE", "1") != "0"
+_CACHE_BYTES = int(os.environ.get("PMM_CORPUS_CACHE_BYTES", str(32 << 30)))
+_CACHE_MIN_BYTES = 1 << 20  # small corpora are cheaper to upload than to cache
+
+
+def _arrow_key(arr):
+    if not isinstance(arr, pa.Array):
+        return None
+    bufs = tuple((b.address, b.size) if b is not None else None for b in arr.buffers())
+    return (str(arr.type), arr.offset, len(arr), bufs)
+
+
+def _cached_corpus(rv, c: np.ndarray):
+    key = _arrow_key(rv)
+    if not _CACHE_ON or key is None or c.nbytes < _CACHE_MIN_BYTES:
+        return None
+    with _cache_lock:
+        hit = _cache.get(key)
+        if hit is not None:
+            _cache.move_to_end(key)
+            return hit[1]
+        dc = _native.DeviceCorpus(c)
+        _cache[key] = (rv, dc)
+        total = sum(v[1].nbytes for v in _cache.values())
+        while total > _CACHE_BYTES and len(_cache) > 1:
+            _, (_, old) = _cache.popitem(last=False)
+            total -= old.nbytes
+            old.close()
+        return dc
+
+
+def clear_corpus_cache() -> None:
+    with _cache_lock:
+        while _cache:
+            _, (_, dc) = _cache.popitem()
+            dc.close()
+
+
+# ---------------------------------------------------------------------------
 # Output builders
 # ---------------------------------------------------------------------------
 _TOPK_STRUCT = pa.struct([("index", pa.uint32()), ("score", pa.float64())])
@@ -221,7 +274,11 @@ def _topk(left, right, k, metric):
         idx = np.zeros((m, 0), dtype=np.uint32)
         sc = np.zeros((m, 0), dtype=np.float64)
     else:
-        idx, sc = _native.topk_host(q, c, kk, metric_id)
+        dc = _cached_corpus(rv, c) if use_f32 else None
+        if dc is not None:
+            idx, sc = dc.topk(q, kk, metric_id)
+        else:
+            idx, sc = _native.topk_host(q, c, kk, metric_id)
         sc = sc.astype(np.float64, copy=False)  # src/matmul.rs:447 (f32 -> f64)
     return _wrap(_topk_arrow(idx, sc, m, kk), "topk", polars_out)
 
@@ -246,4 +303,4 @@ def _matmul(left, right):
     return _wrap(arr, "matmul", polars_out)
 
 
-__all__ = ["_matmul", "_topk", "PanicException"]
+__all__ = ["_matmul", "_topk", "PanicException", "clear_corpus_cache"]

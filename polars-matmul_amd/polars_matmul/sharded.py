@@ -28,6 +28,18 @@ def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
     return n * rank // world, n * (rank + 1) // world
 
 
+def zero_padded(t: torch.Tensor) -> torch.Tensor:
+    """A (rows, d) view whose row stride is roundup(d, 32) with zero-filled
+    padding columns, as pmm_topk_f32_device requires (include/pmm.h)."""
+    rows, d = t.shape
+    dp = -(-d // 32) * 32
+    if d == dp and t.is_contiguous():
+        return t
+    buf = torch.zeros((rows, dp), dtype=t.dtype, device=t.device)
+    buf[:, :d] = t
+    return buf[:, :d]
+
+
 def _device_topk(q: torch.Tensor, c: torch.Tensor, k: int, metric: int, index_base: int,
                  out_i: torch.Tensor, out_s: torch.Tensor, workspace: Optional[torch.Tensor]) -> None:
     from . import _native
@@ -65,6 +77,8 @@ class ShardedTopK:
                  metric: int, group=None,
                  local_topk: Optional[Callable] = None, merge: Optional[Callable] = None,
                  workspace: Optional[torch.Tensor] = None):
+        if local_topk is None:
+            queries, corpus_shard = zero_padded(queries), zero_padded(corpus_shard)
         self.q = queries
         self.c = corpus_shard
         self.index_base = int(index_base)

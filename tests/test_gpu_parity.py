@@ -298,3 +298,61 @@ def test_device_api_sharded_merge_equals_full(pmm):
     got_s = ms.cpu().numpy()
     assert exact_match_rate(got_i, full_i) >= 0.99
     np.testing.assert_allclose(got_s, full_s, rtol=1e-6, atol=1e-6)
+
+
+def test_device_corpus_handle_matches_host_api(pmm):
+    # corpus uploaded once, many calls
+    n = _native()
+    rs = np.random.RandomState(21)
+    q = rs.randn(150, 70).astype(np.float32)
+    c = rs.randn(4000, 70).astype(np.float32)
+    dc = n.DeviceCorpus(c)
+    for metric in ("cosine", "dot", "euclidean"):
+        want = gpu_topk(q, c, 33, metric)
+        got = dc.topk(q, 33, METRICS[metric])
+        assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    dc.close()
+
+
+def test_device_api_logical_d_matches_host_api(pmm):
+    # device API with d = 70 (not a multiple of 32 or 8): rows zero-padded to
+    # a stride of 96, norms over exactly 70 elements -> bit-identical to the
+    # host API, which pads internally
+    import torch
+    from polars_matmul.sharded import ShardedTopK
+
+    rs = np.random.RandomState(23)
+    q = rs.randn(90, 70).astype(np.float32)
+    c = rs.randn(3000, 70).astype(np.float32)
+    dev = torch.device("cuda:0")
+    for metric in ("cosine", "dot", "euclidean"):
+        st = ShardedTopK(torch.from_numpy(q).to(dev), torch.from_numpy(c).to(dev), 0, 17,
+                         METRICS[metric])
+        assert st.q.stride(0) == 96 and st.q.shape[1] == 70
+        oi, osc = st.run()
+        torch.cuda.synchronize()
+        want = gpu_topk(q, c, 17, metric)
+        assert np.array_equal(oi.cpu().numpy().view(np.uint32), want[0])
+        assert np.array_equal(osc.cpu().numpy(), want[1])
+
+
+def test_arrow_corpus_cache_through_extension(pmm):
+    from polars_matmul import _polars_matmul as ext
+
+    ext.clear_corpus_cache()
+    rs = np.random.RandomState(22)
+    c = rs.randn(6000, 64).astype(np.float32)  # 1.5 MB: cached
+    carr = pa.FixedSizeListArray.from_arrays(pa.array(c.reshape(-1)), 64)
+    q1 = pa.FixedSizeListArray.from_arrays(pa.array(rs.randn(40 * 64).astype(np.float32)), 64)
+    q2 = pa.FixedSizeListArray.from_arrays(pa.array(rs.randn(30 * 64).astype(np.float32)), 64)
+    r1 = ext._topk(q1, carr, 12, "cosine")
+    assert len(ext._cache) == 1
+    r2 = ext._topk(q2, carr, 12, "cosine")
+    assert len(ext._cache) == 1  # second batch hits the device-resident corpus
+    for qa, r in ((q1, r1), (q2, r2)):
+        qn = np.asarray(qa.values).reshape(-1, 64)
+        want_i, want_s = gpu_topk(qn, c, 12, "cosine")
+        got = r.to_pylist()
+        assert [[x["index"] for x in row] for row in got] == want_i.tolist()
+    ext.clear_corpus_cache()
+    assert len(ext._cache) == 0
