@@ -39,12 +39,13 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 CONFIGS = {
-    # name: (M, N, D, k, metric)
-    "c3": (100_000, 1_000_000, 768, 100, "cosine"),
-    "c2": (1_000, 10_000, 256, 10, "dot"),
-    "c1": (1_000, 10_000, 256, 10, "cosine"),
+    # name: (M, N, D, k, metric, compute dtype)
+    "c3": (100_000, 1_000_000, 768, 100, "cosine", "f32"),
+    "c4": (100_000, 1_000_000, 768, 100, "cosine", "bf16"),
+    "c2": (1_000, 10_000, 256, 10, "dot", "f32"),
+    "c1": (1_000, 10_000, 256, 10, "cosine", "f32"),
 }
-F32_MFMA_PEAK_TFLOPS = 157.3  # MI355X dense FP32 matrix (MI355X_MICROARCH.md)
+MFMA_PEAK_TFLOPS = {"f32": 157.3, "bf16": 2516.6}  # MI355X dense matrix peaks (MI355X_MICROARCH.md)
 
 
 def log(*a):
@@ -79,6 +80,35 @@ def cpu_baseline(q_dev, c_dev, k, metric, n_sample, threads):
     return n_sample / dt, dt
 
 
+def boundary_rates(q_dev, c_dev, k, metric_id, compute=0):
+    """Host-boundary rates: host f32 buffers in, host idx/score
+    out, through the C ABI, one call each (untimed by the contract's clock):
+      host_api: pmm_topk_f32 -- pads+uploads Q and C, computes, downloads;
+      cached_corpus: pmm_topk_f32_corpus -- corpus resident (uploaded once,
+        as the Arrow-keyed cache does across map_batches calls), Q uploaded
+        and results downloaded per call."""
+    from polars_matmul import _native
+
+    qh = q_dev.cpu().numpy()
+    ch = c_dev.cpu().numpy()
+    M = qh.shape[0]
+    out = {}
+    t0 = time.perf_counter()
+    _native.topk_host(qh, ch, k, metric_id, compute=compute)
+    out["host_api_qps"] = round(M / (time.perf_counter() - t0), 2)
+    if compute != _native.COMPUTE_F32:
+        return out  # the corpus handle is f32-only
+    t0 = time.perf_counter()
+    dc = _native.DeviceCorpus(ch)
+    out["corpus_upload_s"] = round(time.perf_counter() - t0, 3)
+    dc.topk(qh[:1024], k, metric_id)  # first-call allocations
+    t0 = time.perf_counter()
+    dc.topk(qh, k, metric_id)
+    out["cached_corpus_qps"] = round(M / (time.perf_counter() - t0), 2)
+    dc.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -88,6 +118,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=512,
                     help="queries timed on the CPU baseline vs the full corpus (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 torch top-k")
     args = ap.parse_args()
 
@@ -108,7 +139,9 @@ def main():
 
     _native.check(_native.lib().pmm_set_device(torch.cuda.current_device()))
 
-    M, N, D, k, metric = CONFIGS[args.config]
+    M, N, D, k, metric, cdt = CONFIGS[args.config]
+    bf16 = cdt == "bf16"
+    compute = _native.COMPUTE_BF16 if bf16 else _native.COMPUTE_F32
     mid = _native.metric_from_str(metric)
     lo = N * rank // world
     hi = N * (rank + 1) // world
@@ -119,7 +152,11 @@ def main():
     q = torch.randn((M, D), generator=g, device=dev, dtype=torch.float32)
     g.manual_seed(1_000_003 + rank)
     c = torch.randn((n_loc, D), generator=g, device=dev, dtype=torch.float32)
-    ws_bytes = _native.workspace_bytes(M, n_loc, D, k, mid)
+    if bf16:
+        # BASELINE configs[3]: the same f32 embeddings rounded to bf16 (RNE) on
+        # device, resident before the timed region
+        q, c = q.to(torch.bfloat16), c.to(torch.bfloat16)
+    ws_bytes = _native.workspace_bytes(M, n_loc, D, k, mid, compute)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     from polars_matmul.sharded import ShardedTopK
 
@@ -144,7 +181,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     _native.timing_enable(False)
-    kern_ms, kern_n = _native.timing_read("gemm_f32_topk")
+    kern_ms, kern_n = _native.timing_read("gemm_bf16_topk" if bf16 else "gemm_f32_topk")
     merge_ms, merge_n = _native.timing_read("merge_topk")
     shard_ms, shard_n = _native.timing_read("merge_shards")
     if dist:
@@ -175,6 +212,11 @@ def main():
         }
         log(f"spot check: {check}")
 
+    boundary = None
+    if args.boundary and world == 1:
+        boundary = boundary_rates(q.float(), c.float(), k, mid, compute)
+        log(f"boundary: {boundary}")
+
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -185,13 +227,14 @@ def main():
     flops_launch = 2.0 * M * n_loc * D
     avg_kern_s = (kern_ms / kern_n / 1000.0) if kern_n else None
     achieved = flops_launch / avg_kern_s / 1e12 if avg_kern_s else None
+    peak = MFMA_PEAK_TFLOPS[cdt]
     roofline = {
         "bound": "mfma",
-        "kernel": "gemm_f32_kernel (fused GEMM + metric + top-k)",
+        "kernel": f"gemm_{cdt}_kernel (fused GEMM + metric + top-k)",
         "achieved": round(achieved, 2) if achieved else None,
-        "peak": F32_MFMA_PEAK_TFLOPS,
+        "peak": peak,
         "unit": "TFLOP/s",
-        "frac": round(achieved / F32_MFMA_PEAK_TFLOPS, 4) if achieved else None,
+        "frac": round(achieved / peak, 4) if achieved else None,
         "traffic": load_traffic(args.config),
         "kernel_ms_avg": round(kern_ms / kern_n, 3) if kern_n else None,
         "flops_per_launch": flops_launch,
@@ -201,13 +244,14 @@ def main():
     cpu = None
     if args.cpu_sample and world == 1:
         n_s = min(args.cpu_sample, M)
+        # bf16: the oracle on the bf16-rounded rows (widened to f32, exact)
         cpu_qps, cpu_dt = cpu_baseline(q, c, k, metric, n_s, args.cpu_threads)
         cpu = {
             "value": round(cpu_qps, 2),
             "unit": "queries/s",
             "cores": args.cpu_threads,
             "kind": "port",
-            "sample": f"first {n_s} queries x full {N}-row corpus, {D}d f32 {metric} k={k}; "
+            "sample": f"first {n_s} queries x full {N}-row corpus, {D}d {cdt} {metric} k={k}; "
                       f"oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select), {cpu_dt:.1f}s",
         }
     line = {
@@ -221,13 +265,15 @@ def main():
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic N(0,1) f32 embeddings generated on device (torch.randn, seeded)",
-        "config": {"workload": f"{M}x{N}x{D} f32 {metric} k={k} ({args.config})", "queries": M,
+        "dtype": cdt,
+        "data": "synthetic N(0,1) f32 embeddings generated on device (torch.randn, seeded)"
+                + (", rounded to bf16 on device" if bf16 else ""),
+        "config": {"workload": f"{M}x{N}x{D} {cdt} {metric} k={k} ({args.config})", "queries": M,
                    "corpus": N, "dim": D, "k": k, "metric": metric,
                    "parallelism": f"corpus-row-shard x{world}" if world > 1 else "single GPU"},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "boundary": boundary,
         "check": check,
     }
     print(json.dumps(line), flush=True)

@@ -44,8 +44,10 @@ extern "C" {
 
 /* Arithmetic the top-k GEMM runs in (f32 inputs).  F32 = exact f32 MFMA
  * (v_mfma_f32_32x32x2_f32), the reference's precision.  BF16 = inputs rounded
- * to bf16 (RNE) on device, f32 accumulate (v_mfma_f32_32x32x16_bf16); scores
- * of the returned rows are recomputed exactly in f32. */
+ * to bf16 (round to nearest even) on device, products accumulated in f32
+ * (v_mfma_f32_32x32x16_bf16), norms of the rounded rows in f32: the result is
+ * the top-k of the bf16-rounded embeddings (BASELINE configs[3]); limits
+ * d <= 768 and k <= 960 (PMM_ERR_UNSUPPORTED beyond). */
 #define PMM_COMPUTE_F32 0
 #define PMM_COMPUTE_BF16 1
 
@@ -107,7 +109,8 @@ int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64
  * Used by the benchmark and the multi-GPU (corpus-sharded) path.
  * ------------------------------------------------------------------------- */
 
-/* Scratch bytes pmm_topk_f32_device needs for this problem. */
+/* Scratch bytes pmm_topk_f32_device (compute F32) or pmm_topk_bf16_device
+ * (compute BF16) needs for this problem. */
 size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int metric,
                                 int compute);
 
@@ -124,6 +127,16 @@ int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, 
                         int64_t n, int64_t d, int64_t k, int metric, int compute,
                         uint32_t index_base, uint32_t *out_idx, float *out_score,
                         void *workspace, size_t workspace_bytes, void *stream);
+
+/* The bf16 compute path over device-resident bf16 rows (bit patterns, e.g. a
+ * torch.bfloat16 tensor): d is the logical dimension; ldq / ldc >=
+ * roundup(d, 128), multiples of 8, columns past d zero-filled, 16-byte-aligned
+ * bases; d <= 768, k <= 960.  Scores are f32 (see PMM_COMPUTE_BF16); k may
+ * exceed n as in pmm_topk_f32_device. */
+int pmm_topk_bf16_device(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c,
+                         int64_t ldc, int64_t n, int64_t d, int64_t k, int metric,
+                         uint32_t index_base, uint32_t *out_idx, float *out_score,
+                         void *workspace, size_t workspace_bytes, void *stream);
 
 /* k-way merge of per-shard top-k lists: idx/score are [m][lists][k_in] (each
  * list best-first, as pmm_topk_f32_device writes them; idx 0xFFFFFFFF marks

@@ -214,13 +214,21 @@ int choose_variant(int mode, int capg) {
   return 0;
 }
 
-int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p) {
+// compute = PMM_COMPUTE_F32: the f32 kernel (variant chosen by LDS fit);
+// PMM_COMPUTE_BF16: the bf16 kernel (variant -1, 128 x 128 tiles, 4 waves).
+int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p,
+              int compute = PMM_COMPUTE_F32) {
   p.capg = next_pow2((int)k + 64, 128);
-  p.variant = choose_variant(0, p.capg);
+  const bool bf16 = compute == PMM_COMPUTE_BF16;
+  p.variant = bf16 ? -1 : choose_variant(0, p.capg);
+  const int bm = bf16 ? kBf16BM : gemm_f32_bm(p.variant);
+  const int bn = bf16 ? kBf16BN : gemm_f32_bn(p.variant);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
   const size_t cand_budget = size_t(8) << 30;
   int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
-  plan_units(m, n, gemm_f32_bm(p.variant), gemm_f32_bn(p.variant), cus, 0.5, max_S, p);
+  // a bf16 unit starts by loading its 128 query rows into registers (about
+  // two tiles' worth of time): longer splits amortise it
+  plan_units(m, n, bm, bn, cus, bf16 ? 2.0 : 0.5, max_S, p);
   p.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
   size_t off = 0;
   p.off_counter = off;
@@ -236,8 +244,7 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   p.off_cn = off;  // [norms n | inverse norms n]
   off = al256(off + (metric != kMetricDot ? (size_t)n * 8 : 0));
   p.off_wq = off;  // per-wave survivor queues: grid x waves x (32 x BN) u64
-  off = al256(off + (size_t)p.grid * (gemm_f32_bm(p.variant) / 32) * 32 *
-                        gemm_f32_bn(p.variant) * 8);
+  off = al256(off + (size_t)p.grid * (bm / 32) * 32 * bn * 8);
   p.total = off;
   (void)d;
   return PMM_OK;
@@ -439,6 +446,93 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
   return PMM_OK;
 }
 
+// bf16 compute path over device bf16 rows (row strides ldq / ldc >=
+// roundup(d, 128), zero-padded); d is the logical dimension.
+int bf16_limits(int64_t d, int64_t k) {
+  if (cdiv(d, kBf16DAlign) * kBf16DAlign > kBf16MaxD)
+    return fail(PMM_ERR_UNSUPPORTED, "bf16 compute supports d <= %d (got %lld)", kBf16MaxD,
+                (long long)d);
+  if (next_pow2((int)std::min<int64_t>(k, 1 << 20) + 64, 128) > kBf16MaxCapg)
+    return fail(PMM_ERR_UNSUPPORTED, "bf16 compute supports k <= %d (got %lld)", kBf16MaxCapg - 64,
+                (long long)k);
+  return PMM_OK;
+}
+
+int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c,
+                          int64_t ldc, int64_t n, int64_t d, int64_t k, int metric,
+                          uint32_t index_base, uint32_t *out_idx, float *out_score, void *ws,
+                          size_t ws_bytes, hipStream_t s, int dev) {
+  const int cus = g_dev[dev].cus;
+  const int64_t dp = cdiv(d, kBf16DAlign) * kBf16DAlign;
+  Plan p;
+  plan_topk(m, n, dp, k, metric, cus, p, PMM_COMPUTE_BF16);
+  if (!ws) {
+    int rc = arena(dev, s, p.total, &ws);
+    if (rc) return rc;
+  } else if (ws_bytes < p.total) {
+    return fail(PMM_ERR_ARG, "workspace too small: %zu < %zu bytes", ws_bytes, p.total);
+  }
+  char *w = (char *)ws;
+  float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
+  HIP_TRY(hipMemsetAsync(w, 0, p.off_gthr + (size_t)m * 8, s));
+  if (metric != kMetricDot) {
+    const int sq = metric == kMetricEuclidean;
+    Timed t("norms_bf16", s);
+    HIP_TRY(launch_norms_bf16(q, m, d, ldq, sq, qn, nullptr, s));
+    HIP_TRY(launch_norms_bf16(c, n, d, ldc, sq, cn, cn + n, s));
+  }
+  GemmF32Args a{};
+  a.qb = q;
+  a.cb = c;
+  a.qn = qn;
+  a.cn = cn;
+  a.cpre = cn + n;
+  a.ldq = ldq;
+  a.ldc = ldc;
+  a.M = (int)m;
+  a.N = (int)n;
+  a.D = (int)dp;
+  a.k = (int)k;
+  a.capg = p.capg;
+  a.metric = metric;
+  a.QB = p.QB;
+  a.S = p.S;
+  a.tps = p.tps;
+  a.ntiles = p.T;
+  a.units = p.units;
+  a.counter = (unsigned *)(w + p.off_counter);
+  {
+    static const int ablate = getenv("PMM_ABLATE") ? atoi(getenv("PMM_ABLATE")) : 0;
+    a.ablate = ablate;
+  }
+  a.cand = (unsigned long long *)(w + p.off_cand);
+  a.wq = (unsigned long long *)(w + p.off_wq);
+  a.cnt = (unsigned *)(w + p.off_cnt);
+  a.gthr = (unsigned long long *)(w + p.off_gthr);
+  {
+    Timed t("gemm_bf16_topk", s);
+    HIP_TRY(launch_gemm_bf16(a, p.grid, s));
+  }
+  MergeArgs ma{};
+  ma.cand = a.cand;
+  ma.cnt = a.cnt;
+  ma.gthr = a.gthr;
+  ma.capg = p.capg;
+  ma.M = (int)m;
+  ma.S = p.S;
+  ma.k_out = (int)k;
+  ma.P = p.P;
+  ma.metric = metric;
+  ma.index_base = index_base;
+  ma.out_idx = out_idx;
+  ma.out_score = out_score;
+  {
+    Timed t("merge_topk", s);
+    HIP_TRY(launch_merge(ma, 0, s));
+  }
+  return PMM_OK;
+}
+
 // Upload a host matrix rows x d into a device buffer with row stride dp,
 // zero-padding columns d..dp-1.
 int upload_padded(void *dst, const void *src, int64_t rows, int64_t d, int64_t dp, size_t elem,
@@ -521,12 +615,16 @@ int pmm_set_device(int device) {
 
 size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int metric,
                                 int compute) {
-  (void)compute;
   int cus = 256;
   int dev = 0;
   if (hipGetDevice(&dev) == hipSuccess) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     if ((int)g_dev.size() > dev && g_dev[dev].probed) cus = g_dev[dev].cus;
+  }
+  if (compute == PMM_COMPUTE_BF16) {
+    Plan p;
+    plan_topk(m, n, d, k, metric, cus, p, PMM_COMPUTE_BF16);
+    return p.total;
   }
   if (k <= kFusedMaxK) {
     Plan p;
@@ -547,8 +645,11 @@ int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, 
   int rc = validate_sizes(m, n, d, k, true, k <= kFusedMaxK);
   if (rc) return rc;
   if ((rc = check_metric(metric))) return rc;
+  if (compute == PMM_COMPUTE_BF16)
+    return fail(PMM_ERR_UNSUPPORTED,
+                "device f32 inputs with bf16 compute: convert to bf16 and call pmm_topk_bf16_device");
   if (compute != PMM_COMPUTE_F32)
-    return fail(PMM_ERR_UNSUPPORTED, "compute mode %d not available in this build", compute);
+    return fail(PMM_ERR_UNSUPPORTED, "unknown compute mode %d", compute);
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   const int64_t dp = cdiv(d, 32) * 32;
@@ -570,15 +671,40 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
   int rc = validate_sizes(m, n, d, k, true);
   if (rc) return rc;
   if ((rc = check_metric(metric))) return rc;
-  if (compute != PMM_COMPUTE_F32)
-    return fail(PMM_ERR_UNSUPPORTED, "compute mode %d not available in this build", compute);
+  if (compute != PMM_COMPUTE_F32 && compute != PMM_COMPUTE_BF16)
+    return fail(PMM_ERR_UNSUPPORTED, "unknown compute mode %d", compute);
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  if (compute == PMM_COMPUTE_BF16 && (rc = bf16_limits(d, k))) return rc;
   int dev;
   if ((rc = ensure_device(&dev))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
+  if (compute == PMM_COMPUTE_BF16) {
+    // f32 rows uploaded as they are, rounded to zero-padded bf16 rows on device
+    const int64_t db = cdiv(d, kBf16DAlign) * kBf16DAlign;
+    size_t ws_need = pmm_topk_workspace_bytes(m, n, db, k, metric, compute);
+    size_t off_qf = 0, off_cf = al256((size_t)m * d * 4);
+    size_t off_qb = off_cf + al256((size_t)n * d * 4), off_cb = off_qb + al256((size_t)m * db * 2);
+    size_t off_i = off_cb + al256((size_t)n * db * 2), off_s = off_i + al256((size_t)m * k * 4);
+    size_t off_w = off_s + al256((size_t)m * k * 4);
+    void *base;
+    if ((rc = arena(dev, s, off_w + ws_need, &base))) return rc;
+    char *b = (char *)base;
+    HIP_TRY(hipMemcpyAsync(b + off_qf, q, (size_t)m * d * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b + off_cf, c, (size_t)n * d * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_f32_to_bf16((const float *)(b + off_qf), m, d, d, (uint16_t *)(b + off_qb), db, s));
+    HIP_TRY(launch_f32_to_bf16((const float *)(b + off_cf), n, d, d, (uint16_t *)(b + off_cb), db, s));
+    rc = topk_bf16_device_impl((const uint16_t *)(b + off_qb), db, m, (const uint16_t *)(b + off_cb),
+                               db, n, d, k, metric, 0u, (uint32_t *)(b + off_i),
+                               (float *)(b + off_s), b + off_w, ws_need, s, dev);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return PMM_OK;
+  }
   const int64_t dp = cdiv(d, 32) * 32;
   size_t ws_need = pmm_topk_workspace_bytes(m, n, dp, k, metric, compute);
   size_t off_q = 0, off_c = al256((size_t)m * dp * 4), off_i = off_c + al256((size_t)n * dp * 4);
@@ -596,6 +722,31 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
   HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   return PMM_OK;
+}
+
+int pmm_topk_bf16_device(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c,
+                         int64_t ldc, int64_t n, int64_t d, int64_t k, int metric,
+                         uint32_t index_base, uint32_t *out_idx, float *out_score,
+                         void *workspace, size_t workspace_bytes, void *stream) {
+  int rc = validate_sizes(m, n, d, k, true, true);
+  if (rc) return rc;
+  if ((rc = check_metric(metric))) return rc;
+  if (m == 0 || k == 0) return PMM_OK;
+  if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
+  if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  if ((rc = bf16_limits(d, k))) return rc;
+  const int64_t dp = cdiv(d, kBf16DAlign) * kBf16DAlign;
+  if (ldq % 8 != 0 || ldc % 8 != 0 || ldq < dp || ldc < dp || ((uintptr_t)q & 15) ||
+      ((uintptr_t)c & 15))
+    return fail(PMM_ERR_ARG,
+                "bf16 device inputs need row strides >= roundup(d, 128) (zero-padded), multiples "
+                "of 8, 16-byte-aligned bases (d=%lld ldq=%lld ldc=%lld)",
+                (long long)d, (long long)ldq, (long long)ldc);
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s = (hipStream_t)stream;  // NULL = the HIP default stream
+  return topk_bf16_device_impl(q, ldq, m, c, ldc, n, d, k, metric, index_base, out_idx, out_score,
+                               workspace, workspace_bytes, s, dev);
 }
 
 int pmm_topk_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d, int64_t k,

@@ -1,0 +1,272 @@
+// pmm_device.h -- device-side building blocks shared by the gfx950 kernels
+// (pmm_kernels.hip: f32 / f64 paths; pmm_bf16.hip: bf16 compute path):
+// ordered selection keys, wave primitives, the reference-order norms and
+// epilogue arithmetic, the pre-filter bound, buffer-resource LDS-DMA helpers
+// and candidate-buffer compaction.  Not installed.
+#pragma once
+#include "pmm_internal.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace pmm {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef unsigned long long u64;
+
+#define LDS_AS __attribute__((address_space(3)))
+#define GLB_AS __attribute__((address_space(1)))
+
+// ===========================================================================
+// Ordered keys.  The selection order is a total order on (score, index):
+// best score first, NaN last, equal scores -> lower corpus index first.  A
+// score maps to an unsigned key that is monotone in the ranking value
+// (score for cosine/dot, -distance for euclidean); -0 folds onto +0 and NaN
+// maps to 0.  A candidate is the 64-bit composite (key << 32) | ~index, so a
+// single unsigned compare implements the whole order and every composite in
+// a row is unique.
+// ===========================================================================
+__device__ __forceinline__ uint32_t okey32(float v) {
+  if (v != v) return 0u;
+  uint32_t u = __float_as_uint(v);
+  if ((u << 1) == 0u) u = 0u;
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float dekey32(uint32_t k) {
+  if (k == 0u) return __uint_as_float(0x7FC00000u);
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+__device__ __forceinline__ u64 okey64(double v) {
+  if (v != v) return 0ull;
+  u64 u = (u64)__double_as_longlong(v);
+  if ((u << 1) == 0ull) u = 0ull;
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double dekey64(u64 k) {
+  if (k == 0ull) return __longlong_as_double(0x7FF8000000000000ll);
+  return __longlong_as_double((long long)((k & 0x8000000000000000ull) ? (k & 0x7FFFFFFFFFFFFFFFull) : ~k));
+}
+
+// ===========================================================================
+// Wave primitives (wave64).
+// ===========================================================================
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ int lanes_below(u64 mask) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// Bitonic sort, best (largest) first, of P (power of two) u64 in LDS by one wave.
+__device__ inline void wave_sort_desc_u64(u64 *s, int P, int lane) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < (P >> 1); i += 64) {
+        const int x0 = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
+        const int x1 = x0 + stride;
+        const u64 a = s[x0], b = s[x1];
+        const bool desc = (x0 & size) == 0;
+        if (desc ? (a < b) : (a > b)) {
+          s[x0] = b;
+          s[x1] = a;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
+// 16-byte entry for the materialised (row-select) path: f64 keys need all
+// 64 bits, so the index rides alongside.
+struct __attribute__((aligned(16))) Ent {
+  u64 key;
+  uint32_t idx;
+  uint32_t pad;
+};
+__device__ __forceinline__ bool ent_better(const Ent &a, const Ent &b) {
+  return a.key > b.key || (a.key == b.key && a.idx < b.idx);
+}
+__device__ inline void wave_sort_desc_ent(Ent *s, int P, int lane) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < (P >> 1); i += 64) {
+        const int x0 = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
+        const int x1 = x0 + stride;
+        const Ent a = s[x0], b = s[x1];
+        const bool desc = (x0 & size) == 0;
+        if (desc ? ent_better(b, a) : ent_better(a, b)) {
+          s[x0] = b;
+          s[x1] = a;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
+__device__ __forceinline__ int next_pow2_dev(int x) {
+  int p = 64;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+// ===========================================================================
+// Row norms in ndarray's `unrolled_dot` order (src/metrics.rs:368-393 ->
+// ndarray 0.16 unrolled_dot): accumulator j sums x[8t+j]^2 sequentially,
+// combined as ((((0+(p0+p4))+(p1+p5))+(p2+p6))+(p3+p7)) then the scalar tail.
+// 8 lanes per row, lane j owns accumulator p_j -> bit-identical to the
+// reference's norms (no FMA: the file is built with -ffp-contract=off).
+// ===========================================================================
+template <typename T>
+__device__ __forceinline__ T sqrt_rn(T x);
+template <>
+__device__ __forceinline__ float sqrt_rn<float>(float x) { return __fsqrt_rn(x); }
+template <>
+__device__ __forceinline__ double sqrt_rn<double>(double x) { return __dsqrt_rn(x); }
+
+// TI = stored element type (f32, f64, or bf16 for the bf16 compute path, whose
+// norms are those of the bf16-rounded rows, accumulated in f32).
+template <typename T, typename TI = T>
+__global__ __launch_bounds__(256) void norms_kernel(const TI *__restrict__ a, int64_t rows,
+                                                    int64_t d, int64_t ld, int squared,
+                                                    T *__restrict__ out, T *__restrict__ inv) {
+  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = gt >> 3;
+  const int j = threadIdx.x & 7;
+  const bool valid = row < rows;
+  const TI *p = a + (valid ? row : 0) * ld;
+  const int64_t d8 = d & ~(int64_t)7;
+  T acc = (T)0;
+  if (valid) {
+    for (int64_t i = j; i < d8; i += 8) {
+      const T x = (T)p[i];
+      acc = acc + x * x;
+    }
+  }
+  const int base = (int)(threadIdx.x & 63) & ~7;
+  T pp[8];
+#pragma unroll
+  for (int t = 0; t < 8; t++) pp[t] = __shfl(acc, base + t, 64);
+  if (valid && j == 0) {
+    T sum = (T)0;
+    sum = sum + (pp[0] + pp[4]);
+    sum = sum + (pp[1] + pp[5]);
+    sum = sum + (pp[2] + pp[6]);
+    sum = sum + (pp[3] + pp[7]);
+    for (int64_t i = d8; i < d; i++) {
+      const T x = (T)p[i];
+      sum = sum + x * x;
+    }
+    const T v = squared ? sum : sqrt_rn<T>(sum);
+    out[row] = v;
+    // pre-filter column factor (see prefilter_bound): cosine 1/norm (0 for the
+    // reference's zero-norm rule); euclidean the squared norm shrunk by 2^-18
+    // so 2*dot - factor over-estimates qsq - sq by more than its rounding.
+    if (inv) inv[row] = squared ? v * (T)(1.0 - 0x1p-18) : ((v > (T)1e-6) ? (T)1 / v : (T)0);
+  }
+}
+
+// ===========================================================================
+// Epilogue arithmetic, exactly as the reference orders it.
+//   cosine   (metrics.rs:329-343): q>1e-6 && c>1e-6 ? dot / (q*c) : 0
+//   euclid   (metrics.rs:347-362): sqrt(max((qsq + csq) - 2*dot, 0)),
+//            Rust f32::max returns the non-NaN operand -> NaN becomes 0.
+// ===========================================================================
+template <int METRIC>
+__device__ __forceinline__ float exact_score(float dot, float qv, float cv) {
+  if (METRIC == kMetricDot) return dot;
+  if (METRIC == kMetricCosine) {
+    if (qv > 1e-6f && cv > 1e-6f) return __fdiv_rn(dot, __fmul_rn(qv, cv));
+    return 0.0f;
+  }
+  const float sq = __fsub_rn(__fadd_rn(qv, cv), 2.0f * dot);
+  const float mx = (sq > 0.0f) ? sq : 0.0f;
+  return __fsqrt_rn(mx);
+}
+template <int METRIC>
+__device__ __forceinline__ double exact_score_f64(double dot, double qv, double cv) {
+  if (METRIC == kMetricDot) return dot;
+  if (METRIC == kMetricCosine) {
+    if (qv > 1e-10 && cv > 1e-10) return __ddiv_rn(dot, __dmul_rn(qv, cv));
+    return 0.0;
+  }
+  const double sq = __dsub_rn(__dadd_rn(qv, cv), 2.0 * dot);
+  const double mx = (sq > 0.0) ? sq : 0.0;
+  return __dsqrt_rn(mx);
+}
+
+// Pre-filter.  For every score the hot epilogue computes ONE value
+//   dot:    pv = dot                     (exact)
+//   cosine: pv = dot * (1/cn)            (= score * qn within 5 ulp)
+//   euclid: pv = 2*dot - csq*(1-2^-18)   (>= qsq - sq - rounding)
+// and keeps the element iff !(pv < L), with the per-row bound L derived from
+// the row's current k-th composite `thr` and the row norm qv (cosine: ||q||,
+// euclid: ||q||^2).  L is loose by a margin that covers every rounding step,
+// so the pre-filter never rejects a true candidate; survivors are re-scored
+// exactly and compared as composites.  NaN pv always passes (!(NaN < L)).
+template <int METRIC>
+__device__ __forceinline__ float prefilter_bound(u64 thr, float qv) {
+  const float inf = __builtin_inff();
+  if (thr == ~0ull) return inf;                 // padding row: reject all
+  const uint32_t tk = (uint32_t)(thr >> 32);
+  if (tk == 0u) return -inf;                    // row not full: accept all
+  const float v = dekey32(tk);                  // ranking value of the k-th
+  if (METRIC == kMetricDot) return v;
+  if (METRIC == kMetricCosine) {
+    if (!(qv > 1e-6f)) return (0.0f >= v) ? -inf : inf;  // zero-norm row: every score is 0
+    const float lo = v - (fabsf(v) * 0x1p-19f + 0x1p-100f);
+    const float L = lo * qv;
+    return L - (fabsf(L) * 0x1p-20f + 0x1p-100f);
+  }
+  const float dist = -v;
+  const float hi = dist * dist * (1.0f + 0x1p-20f) + 0x1p-100f;
+  const float L = qv - hi;
+  return L - ((fabsf(qv) + hi) * 0x1p-18f + 0x1p-100f);
+}
+
+__device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {
+  const int nrec = bytes <= 0 ? 0 : (int)(bytes > 0x7FFFFFFFll ? 0x7FFFFFFFll : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void *)base, (short)0, nrec, 0x00020000);
+}
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char *lds, uint32_t voff,
+                                      uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void *)lds, 16, voff, soff, 0, 0);
+}
+
+// Wave-level compaction of one row's candidate buffer: sort, keep the best k,
+// raise the row threshold to the k-th composite and publish it (atomicMax)
+// so later units of the same row prune with it.
+__device__ inline void compact_row(const GemmF32Args &a, int s, int grow, u64 *thr_slot,
+                                   unsigned *cnt_slot, u64 *scr, int lane) {
+  u64 *base = a.cand + ((int64_t)grow * a.S + s) * a.capg;
+  const int n = (int)*cnt_slot;
+  const int P = a.capg;
+  for (int i = lane; i < P; i += 64)
+    scr[i] = (i < n) ? __hip_atomic_load(base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : 0ull;
+  wave_sync();
+  wave_sort_desc_u64(scr, P, lane);
+  const int kk = min(a.k, n);
+  for (int i = lane; i < kk; i += 64) base[i] = scr[i];
+  const u64 nt = (n >= a.k) ? scr[a.k - 1] : 0ull;
+  wave_sync();
+  if (lane == 0) {
+    *cnt_slot = (unsigned)kk;
+    if (nt > *thr_slot) *thr_slot = nt;
+    if (nt) atomicMax(a.gthr + grow, nt);
+  }
+  wave_sync();
+}
+
+}  // namespace pmm

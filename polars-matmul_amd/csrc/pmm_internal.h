@@ -22,6 +22,8 @@ constexpr int kRowSelMaxP = 4096;
 struct GemmF32Args {
   const float *q;       // M x ldq
   const float *c;       // N x ldc
+  const uint16_t *qb;   // bf16 compute path: M x ldq bf16 (bit patterns)
+  const uint16_t *cb;   // bf16 compute path: N x ldc bf16
   const float *qn;      // cosine: L2 norms of Q rows; euclidean: squared norms
   const float *cn;      // same for C rows
   const float *cpre;    // pre-filter column factor: cosine 1/||c|| (0 if zero-norm),
@@ -80,6 +82,21 @@ int gemm_f32_bm(int variant);   // query rows per workgroup
 int gemm_f32_bn(int variant);   // corpus columns per tile
 size_t gemm_f32_lds_bytes(int variant, int mode, int capg);
 hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s);
+// ---- bf16 compute path (pmm_bf16.hip) ----
+// Fused top-k on bf16 operands: 128 query rows x 128 corpus columns per
+// workgroup tile, 4 waves (1 per SIMD), query rows register-resident.
+constexpr int kBf16BM = 128, kBf16BN = 128, kBf16NW = 4;
+constexpr int kBf16MaxD = 768;  // padded D (multiple of kBf16DAlign) limit: registers
+constexpr int kBf16DAlign = 128;
+constexpr int kBf16MaxCapg = 1024;  // LDS budget for the compaction scratch (k <= 960)
+hipError_t launch_gemm_bf16(const GemmF32Args &a, int grid, hipStream_t s);
+size_t gemm_bf16_lds_bytes(int capg);
+// f32 rows -> bf16 (round to nearest even) with row stride ldd, columns
+// d..ldd-1 zero-filled.
+hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t lds, uint16_t *dst,
+                              int64_t ldd, hipStream_t s);
+hipError_t launch_norms_bf16(const uint16_t *a, int64_t rows, int64_t d, int64_t ld, int squared,
+                             float *out, float *inv, hipStream_t s);
 size_t merge_lds_bytes_per_wave(int P);
 hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, int64_t ldc,
                                  const double *qn, const double *cn, int M, int N, int D,

@@ -45,6 +45,7 @@ EXPORTED_SYMBOLS = (
     "pmm_matmul_f64",
     "pmm_topk_workspace_bytes",
     "pmm_topk_f32_device",
+    "pmm_topk_bf16_device",
     "pmm_merge_topk_device",
     "pmm_corpus_create_f32",
     "pmm_corpus_destroy",
@@ -93,6 +94,9 @@ _SIGS = {
     "pmm_topk_f32_device": (
         [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _u32, _vp, _vp, _vp, _sz, _vp],
         _i32,
+    ),
+    "pmm_topk_bf16_device": (
+        [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _u32, _vp, _vp, _vp, _sz, _vp], _i32
     ),
     "pmm_merge_topk_device": ([_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp], _i32),
     "pmm_corpus_create_f32": ([_vp, _i64, _i64, ctypes.POINTER(ctypes.c_void_p)], _i32),
@@ -188,6 +192,16 @@ def topk_device(q_ptr: int, ldq: int, m: int, c_ptr: int, ldc: int, n: int, d: i
     check(_lib.pmm_topk_f32_device(q_ptr, ldq, m, c_ptr, ldc, n, d, k, metric, compute,
                                    index_base, out_idx_ptr, out_score_ptr, workspace or None,
                                    workspace_bytes, stream or None))
+
+
+def topk_bf16_device(q_ptr: int, ldq: int, m: int, c_ptr: int, ldc: int, n: int, d: int, k: int,
+                     metric: int, out_idx_ptr: int, out_score_ptr: int, *, index_base: int = 0,
+                     workspace: int = 0, workspace_bytes: int = 0, stream: int = 0) -> None:
+    """Device-resident bf16 top-k (bf16 row bit patterns in HBM, e.g. a
+    torch.bfloat16 tensor's data_ptr()); row strides >= roundup(d, 128)."""
+    check(_lib.pmm_topk_bf16_device(q_ptr, ldq, m, c_ptr, ldc, n, d, k, metric, index_base,
+                                    out_idx_ptr, out_score_ptr, workspace or None, workspace_bytes,
+                                    stream or None))
 
 
 def merge_device(idx_ptr: int, score_ptr: int, m: int, lists: int, k_in: int, k_out: int,

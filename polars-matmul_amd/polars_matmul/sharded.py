@@ -28,11 +28,12 @@ def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
     return n * rank // world, n * (rank + 1) // world
 
 
-def zero_padded(t: torch.Tensor) -> torch.Tensor:
-    """A (rows, d) view whose row stride is roundup(d, 32) with zero-filled
-    padding columns, as pmm_topk_f32_device requires (include/pmm.h)."""
+def zero_padded(t: torch.Tensor, align: int = 32) -> torch.Tensor:
+    """A (rows, d) view whose row stride is roundup(d, align) with zero-filled
+    padding columns, as pmm_topk_f32_device (align 32) and
+    pmm_topk_bf16_device (align 128) require (include/pmm.h)."""
     rows, d = t.shape
-    dp = -(-d // 32) * 32
+    dp = -(-d // align) * align
     if d == dp and t.is_contiguous():
         return t
     buf = torch.zeros((rows, dp), dtype=t.dtype, device=t.device)
@@ -54,6 +55,20 @@ def _device_topk(q: torch.Tensor, c: torch.Tensor, k: int, metric: int, index_ba
                         stream=torch.cuda.current_stream(q.device).cuda_stream)
 
 
+def _device_topk_bf16(q: torch.Tensor, c: torch.Tensor, k: int, metric: int, index_base: int,
+                      out_i: torch.Tensor, out_s: torch.Tensor, workspace: Optional[torch.Tensor]) -> None:
+    from . import _native
+
+    m, d = q.shape
+    n = c.shape[0]
+    ws_ptr = workspace.data_ptr() if workspace is not None else 0
+    ws_bytes = workspace.numel() if workspace is not None else 0
+    _native.topk_bf16_device(q.data_ptr(), q.stride(0), m, c.data_ptr(), c.stride(0), n, d, k, metric,
+                             out_i.data_ptr(), out_s.data_ptr(), index_base=index_base,
+                             workspace=ws_ptr, workspace_bytes=ws_bytes,
+                             stream=torch.cuda.current_stream(q.device).cuda_stream)
+
+
 def _device_merge(lists_i: torch.Tensor, lists_s: torch.Tensor, k: int, metric: int,
                   out_i: torch.Tensor, out_s: torch.Tensor) -> None:
     from . import _native
@@ -67,8 +82,10 @@ def _device_merge(lists_i: torch.Tensor, lists_s: torch.Tensor, k: int, metric: 
 class ShardedTopK:
     """Reusable per-rank state for repeated sharded top-k passes.
 
-    queries: (M, D) f32 tensor (replicated on every rank)
-    corpus_shard: (n_local, D) f32 tensor, rows [index_base, index_base + n_local)
+    queries: (M, D) f32 tensor (replicated on every rank), or bf16 for the
+        bf16 compute path (pmm_topk_bf16_device)
+    corpus_shard: (n_local, D) tensor of the same dtype, rows
+        [index_base, index_base + n_local)
     Returns from ``run()``: (idx int32 (M, k), score f32 (M, k)) on rank 0 (the
     global top-k), the local lists on other ranks.
     """
@@ -78,7 +95,10 @@ class ShardedTopK:
                  local_topk: Optional[Callable] = None, merge: Optional[Callable] = None,
                  workspace: Optional[torch.Tensor] = None):
         if local_topk is None:
-            queries, corpus_shard = zero_padded(queries), zero_padded(corpus_shard)
+            bf16 = queries.dtype == torch.bfloat16
+            align = 128 if bf16 else 32
+            queries, corpus_shard = zero_padded(queries, align), zero_padded(corpus_shard, align)
+            local_topk = _device_topk_bf16 if bf16 else _device_topk
         self.q = queries
         self.c = corpus_shard
         self.index_base = int(index_base)

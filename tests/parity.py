@@ -78,3 +78,15 @@ def dot_scale(q, c):
     q = np.asarray(q, dtype=np.float64)
     c = np.asarray(c, dtype=np.float64)
     return np.outer(np.sqrt((q * q).sum(1)), np.sqrt((c * c).sum(1)))
+
+
+def round_bf16(x: np.ndarray) -> np.ndarray:
+    """f32 -> nearest-even bf16, returned as f32 (the device's v_cvt_pk_bf16_f32
+    for finite inputs; NaN stays NaN)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    u = x.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000).astype(np.uint32)
+    out = r.view(np.float32).copy()
+    nan = np.isnan(x)
+    out[nan] = np.nan
+    return out

@@ -356,3 +356,117 @@ def test_arrow_corpus_cache_through_extension(pmm):
         assert [[x["index"] for x in row] for row in got] == want_i.tolist()
     ext.clear_corpus_cache()
     assert len(ext._cache) == 0
+
+
+# ---------------------------------------------------------------------------
+# bf16 compute path (PMM_COMPUTE_BF16, BASELINE configs[3]).  Truth = the
+# metric of the bf16-rounded rows in float64; the device accumulates the
+# bf16 products in f32, so the f32 tolerance applies (rtol 1e-5 + the
+# |q||c|-scaled dot term).  SURVEY 8c's own bar for bf16 (recall@k >= 0.95
+# vs the f32 result) is checked separately.
+# ---------------------------------------------------------------------------
+def gpu_topk_bf16(q, c, k, metric):
+    n = _native()
+    kk = min(k, c.shape[0])
+    return n.topk_host(np.ascontiguousarray(q, dtype=np.float32),
+                       np.ascontiguousarray(c, dtype=np.float32), kk, METRICS[metric],
+                       compute=n.COMPUTE_BF16)
+
+
+def _bf16_truth_check(q, c, k, metric, idx, sc, label):
+    from golden.make_golden import truth_scores
+    from parity import round_bf16
+
+    qb, cb = round_bf16(q), round_bf16(c)
+    truth = truth_scores(qb, cb, metric)
+    scale = dot_scale(qb, cb) if metric == "dot" else None
+    check_topk(idx, sc, truth, metric != "euclidean", rtol=1e-5, atol=1e-5, scale=scale, label=label)
+
+
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+@pytest.mark.parametrize("k", [1, 10, 100, 900])
+def test_bf16_fixture_vs_bf16_truth(pmm, metric, k):
+    z = np.load(os.path.join(GOLD, "rand_f32_48x1000x256.npz"))
+    idx, sc = gpu_topk_bf16(z["q"], z["c"], k, metric)
+    _bf16_truth_check(z["q"], z["c"], k, metric, idx, sc, f"bf16 {metric} k={k}")
+
+
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_edge_fixture(pmm, metric):
+    # zero-norm rows, exact duplicates (ties -> lower index first), d=37 -> 128
+    z = np.load(os.path.join(GOLD, "edge_f32_6x70x37.npz"))
+    idx, sc = gpu_topk_bf16(z["q"], z["c"], 70, metric)
+    _bf16_truth_check(z["q"], z["c"], 70, metric, idx, sc, f"bf16 edge {metric}")
+    for i in range(6):
+        row = idx[i].tolist()
+        assert row.index(3) < row.index(11) < row.index(40)
+    if metric == "cosine":
+        assert np.all(sc[2] == 0.0) and idx[2].tolist() == list(range(70))
+
+
+@pytest.mark.parametrize("m,n,d,k", [
+    (1, 1, 1, 1), (3, 5, 2, 5), (130, 257, 33, 7), (129, 1000, 128, 100), (7, 300, 768, 16),
+    (257, 4099, 200, 64), (300, 2000, 768, 448),
+])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_ragged_shapes(pmm, m, n, d, k, metric):
+    rs = np.random.RandomState(m * 5 + n + d)
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    idx, sc = gpu_topk_bf16(q, c, k, metric)
+    _bf16_truth_check(q, c, k, metric, idx, sc, f"bf16 {m}x{n}x{d} k={k} {metric}")
+
+
+def test_bf16_recall_vs_f32(pmm):
+    # SURVEY 8c bf16 criterion: recall@k >= 0.95 against the f32 result
+    rs = np.random.RandomState(31)
+    q = rs.randn(200, 768).astype(np.float32)
+    c = rs.randn(20000, 768).astype(np.float32)
+    bi, bs = gpu_topk_bf16(q, c, 100, "cosine")
+    fi, fs = gpu_topk(q, c, 100, "cosine")
+    recall = np.mean([len(set(bi[i]) & set(fi[i])) / 100.0 for i in range(len(q))])
+    assert recall >= 0.95, recall
+    assert np.max(np.abs(bs - fs)) < 1e-2
+
+
+def test_bf16_device_api_many_splits(pmm):
+    # device bf16 rows (torch.bfloat16), a corpus long enough for several
+    # splits and many tiles per unit; truth from float64 on device
+    import torch
+
+    n = _native()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    m, N, d, k = 700, 60000, 768, 100
+    q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
+    c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
+    oi = torch.empty((m, k), dtype=torch.int32, device=dev)
+    osc = torch.empty((m, k), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS["cosine"],
+                       oi.data_ptr(), osc.data_ptr(), index_base=7, stream=stream)
+    torch.cuda.synchronize()
+    qd, cd = q.double(), c.double()
+    s = (qd @ cd.T) / (qd.norm(dim=1, keepdim=True) * cd.norm(dim=1)[None, :])
+    ref_s, ref_i = torch.topk(s, k, dim=1)
+    got_i = oi.long() - 7
+    assert int(got_i.min()) >= 0 and int(got_i.max()) < N
+    got_true = torch.gather(s, 1, got_i)
+    kth = ref_s[:, -1:]
+    assert bool((got_true >= kth - 2e-5).all())
+    assert float((osc.double() - got_true).abs().max()) < 1e-5
+    assert float((got_i == ref_i).float().mean()) > 0.97
+
+
+def test_bf16_limits_raise(pmm):
+    n = _native()
+    q = np.zeros((2, 800), np.float32)
+    with pytest.raises(n.PmmError) as e:
+        n.topk_host(q, q, 1, 0, compute=n.COMPUTE_BF16)
+    assert e.value.code == n.PMM_ERR_UNSUPPORTED and "d <= 768" in str(e.value)
+    q = np.ones((2, 8), np.float32)
+    c = np.ones((1000, 8), np.float32)
+    with pytest.raises(n.PmmError) as e:
+        n.topk_host(q, c, 961, 0, compute=n.COMPUTE_BF16)
+    assert e.value.code == n.PMM_ERR_UNSUPPORTED
