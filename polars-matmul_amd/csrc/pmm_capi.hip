@@ -243,8 +243,8 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   off = al256(off + (metric != kMetricDot ? (size_t)m * 8 : 0));
   p.off_cn = off;  // [norms n | inverse norms n]
   off = al256(off + (metric != kMetricDot ? (size_t)n * 8 : 0));
-  p.off_wq = off;  // per-wave survivor queues: grid x waves x (32 x BN) u64
-  off = al256(off + (size_t)p.grid * (bm / 32) * 32 * bn * 8);
+  p.off_wq = off;  // f32 kernel: per-wave survivor queues, grid x waves x (32 x BN) u64
+  off = al256(off + (bf16 ? 0 : (size_t)p.grid * (bm / 32) * 32 * bn * 8));
   p.total = off;
   (void)d;
   return PMM_OK;
@@ -510,8 +510,35 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
   a.cnt = (unsigned *)(w + p.off_cnt);
   a.gthr = (unsigned long long *)(w + p.off_gthr);
   {
-    Timed t("gemm_bf16_topk", s);
-    HIP_TRY(launch_gemm_bf16(a, p.grid, s));
+    a.nst = 3;  // LDS ring slots of the bf16 kernel
+    static const int sync_env = getenv("PMM_BF16_SYNC") ? atoi(getenv("PMM_BF16_SYNC")) : 1;
+    a.round_sync = sync_env;
+    // round-barrier spin limit: workgroups of one round finish up to a few ms
+    // apart (uneven epilogues); a workgroup that times out stops syncing
+    static const int tmo_env =
+        getenv("PMM_BF16_SYNC_TIMEOUT_US") ? atoi(getenv("PMM_BF16_SYNC_TIMEOUT_US")) : 20000;
+    a.sync_timeout = tmo_env * 100;
+    static const bool stats = getenv("PMM_STATS") != nullptr;
+    static unsigned long long *stats_buf = nullptr;
+    if (stats) {
+      if (!stats_buf) HIP_TRY(hipMalloc(&stats_buf, 64));
+      HIP_TRY(hipMemsetAsync(stats_buf, 0, 64, s));
+      a.stats = stats_buf;
+    }
+    {
+      Timed t("gemm_bf16_topk", s);
+      HIP_TRY(launch_gemm_bf16(a, p.grid, s));
+    }
+    if (stats) {
+      unsigned long long h[8];
+      HIP_TRY(hipMemcpyAsync(h, stats_buf, 64, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      fprintf(stderr,
+              "[pmm stats] gemm_bf16: queued %llu, LDS-queue tiles %llu, sync timeouts %llu, "
+              "compactions %llu, units %d, S %d, tps %d; wave cycles: K-loop %.3g, extract %.3g, "
+              "pass 2 %.3g\n",
+              h[0], h[1], h[2], h[3], p.units, p.S, p.tps, (double)h[4], (double)h[5], (double)h[6]);
+    }
   }
   MergeArgs ma{};
   ma.cand = a.cand;

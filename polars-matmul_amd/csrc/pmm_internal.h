@@ -42,6 +42,10 @@ struct GemmF32Args {
   int64_t ldo;
   int store_metric;               // store mode: 1 = metric-transformed score, 0 = raw dot
   int ablate;                     // benchmarking only (PMM_ABLATE): 1 = skip the epilogue
+  int nst;                        // bf16 kernel: LDS ring slots (3 or 4)
+  int round_sync;                 // bf16 kernel: align workgroups at unit rounds (speed only)
+  int sync_timeout;               // bf16 kernel: round-barrier spin limit (100 MHz ticks)
+  unsigned long long *stats;      // PMM_STATS only: [queued, flagged groups, tiles, compactions]
 };
 
 struct MergeArgs {
@@ -90,7 +94,7 @@ constexpr int kBf16MaxD = 768;  // padded D (multiple of kBf16DAlign) limit: reg
 constexpr int kBf16DAlign = 128;
 constexpr int kBf16MaxCapg = 1024;  // LDS budget for the compaction scratch (k <= 960)
 hipError_t launch_gemm_bf16(const GemmF32Args &a, int grid, hipStream_t s);
-size_t gemm_bf16_lds_bytes(int capg);
+size_t gemm_bf16_lds_bytes(int capg, int nst);
 // f32 rows -> bf16 (round to nearest even) with row stride ldd, columns
 // d..ldd-1 zero-filled.
 hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t lds, uint16_t *dst,
