@@ -109,6 +109,53 @@ def boundary_rates(q_dev, c_dev, k, metric_id, compute=0):
     return out
 
 
+def measure_extra(name, steps, warmup, dev):
+    """Secondary workload on this GPU (N = 1 runs only): the same timing as the
+    main line (inputs resident, K steps bracketed by synchronize), reported
+    under "extra" -- e.g. c4, BASELINE configs[3] (bf16 compute)."""
+    from polars_matmul import _native
+    from polars_matmul.sharded import ShardedTopK
+
+    M, N, D, k, metric, cdt = CONFIGS[name]
+    mid = _native.metric_from_str(metric)
+    bf16 = cdt == "bf16"
+    g = torch.Generator(device=dev)
+    g.manual_seed(42)
+    q = torch.randn((M, D), generator=g, device=dev, dtype=torch.float32)
+    g.manual_seed(1_000_003)
+    c = torch.randn((N, D), generator=g, device=dev, dtype=torch.float32)
+    if bf16:
+        q, c = q.to(torch.bfloat16), c.to(torch.bfloat16)
+    compute = _native.COMPUTE_BF16 if bf16 else _native.COMPUTE_F32
+    ws = torch.empty(_native.workspace_bytes(M, N, D, k, mid, compute), dtype=torch.uint8, device=dev)
+    runner = ShardedTopK(q, c, 0, k, mid, workspace=ws)
+    for _ in range(warmup):
+        runner.run()
+    torch.cuda.synchronize()
+    _native.timing_reset()
+    _native.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        runner.run()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    _native.timing_enable(False)
+    kms, kn = _native.timing_read("gemm_bf16_topk" if bf16 else "gemm_f32_topk")
+    ach = 2.0 * M * N * D / (kms / kn / 1000.0) / 1e12 if kn else None
+    out = {
+        "config": {"workload": f"{M}x{N}x{D} {cdt} {metric} k={k} ({name})"},
+        "dtype": cdt, "value": round(M * steps / el, 2), "unit": "queries/s",
+        "ms_per_step": round(el / steps * 1000.0, 3), "steps": steps, "warmup": warmup,
+        "roofline": {"bound": "mfma", "achieved": round(ach, 2) if ach else None,
+                     "peak": MFMA_PEAK_TFLOPS[cdt], "unit": "TFLOP/s",
+                     "frac": round(ach / MFMA_PEAK_TFLOPS[cdt], 4) if ach else None,
+                     "kernel_ms_avg": round(kms / kn, 3) if kn else None},
+    }
+    del runner, ws, q, c
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +166,8 @@ def main():
                     help="queries timed on the CPU baseline vs the full corpus (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
+    ap.add_argument("--extra", default="c4",
+                    help="comma-separated secondary configs measured after the main line (N=1; '' = none)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 torch top-k")
     args = ap.parse_args()
 
@@ -217,6 +266,15 @@ def main():
         boundary = boundary_rates(q.float(), c.float(), k, mid, compute)
         log(f"boundary: {boundary}")
 
+    extra = None
+    if args.extra and world == 1:
+        del runner, ws
+        torch.cuda.empty_cache()
+        extra = {}
+        for name in [x for x in args.extra.split(",") if x and x != args.config]:
+            extra[name] = measure_extra(name, args.steps, args.warmup, dev)
+            log(f"extra {name}: {extra[name]}")
+
     if rank != 0:
         if dist:
             dist.destroy_process_group()
@@ -274,6 +332,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "boundary": boundary,
+        "extra": extra,
         "check": check,
     }
     print(json.dumps(line), flush=True)

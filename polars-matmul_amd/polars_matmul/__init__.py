@@ -34,6 +34,7 @@ __version__ = "0.1.4"
 __all__ = ["PmmNamespace", "topk", "matmul"]
 
 Metric = Literal["cosine", "dot", "euclidean"]
+Compute = Literal["f32", "bf16"]
 
 try:
     import polars as pl  # type: ignore
@@ -41,13 +42,21 @@ except Exception:  # polars is optional (not installable in this image)
     pl = None
 
 
-def topk(queries: np.ndarray, corpus: np.ndarray, k: int, metric: Metric = "cosine"):
+def topk(queries: np.ndarray, corpus: np.ndarray, k: int, metric: Metric = "cosine",
+         compute: Compute = "f32"):
     """numpy-level top-k: returns (indices uint32 [m, k'], scores float64 [m, k'])
     with k' = min(k, len(corpus)); f32 compute iff both inputs are float32
-    (src/matmul.rs:427), scores widened to f64 (src/matmul.rs:447)."""
+    (src/matmul.rs:427), scores widened to f64 (src/matmul.rs:447).
+    compute="bf16" (an extension, not in the reference): f32 inputs rounded to
+    bf16 on the device, bf16 MFMA with f32 accumulation (include/pmm.h
+    PMM_COMPUTE_BF16: d <= 768, k <= 960)."""
     q = np.asarray(queries)
     c = np.asarray(corpus)
+    if compute not in ("f32", "bf16"):
+        raise ValueError(f"compute must be 'f32' or 'bf16', not {compute!r}")
     dt = np.float32 if (q.dtype == np.float32 and c.dtype == np.float32) else np.float64
+    if compute == "bf16":
+        dt = np.float32
     q = np.ascontiguousarray(q, dtype=dt)
     c = np.ascontiguousarray(c, dtype=dt)
     if q.shape[1] != c.shape[1]:
@@ -56,7 +65,8 @@ def topk(queries: np.ndarray, corpus: np.ndarray, k: int, metric: Metric = "cosi
             f"right has {c.shape[1]} dimensional vectors"
         )
     kk = min(int(k), c.shape[0])
-    idx, sc = _native.topk_host(q, c, kk, _native.metric_from_str(metric))
+    mode = _native.COMPUTE_BF16 if compute == "bf16" else _native.COMPUTE_F32
+    idx, sc = _native.topk_host(q, c, kk, _native.metric_from_str(metric), compute=mode)
     return idx, sc.astype(np.float64, copy=False)
 
 

@@ -470,3 +470,24 @@ def test_bf16_limits_raise(pmm):
     with pytest.raises(n.PmmError) as e:
         n.topk_host(q, c, 961, 0, compute=n.COMPUTE_BF16)
     assert e.value.code == n.PMM_ERR_UNSUPPORTED
+
+
+def test_bf16_numpy_api_and_sharded_runner(pmm):
+    # polars_matmul.topk(compute="bf16") and ShardedTopK over bf16 tensors
+    # (d = 200 -> zero-padded to a 256 stride) agree with each other
+    import torch
+    from polars_matmul.sharded import ShardedTopK
+
+    rs = np.random.RandomState(41)
+    q = rs.randn(77, 200).astype(np.float32)
+    c = rs.randn(2500, 200).astype(np.float32)
+    i1, s1 = pmm.topk(q, c, 25, "euclidean", compute="bf16")
+    _bf16_truth_check(q, c, 25, "euclidean", i1, s1, "bf16 numpy api")
+    dev = torch.device("cuda:0")
+    st = ShardedTopK(torch.from_numpy(q).to(dev).to(torch.bfloat16),
+                     torch.from_numpy(c).to(dev).to(torch.bfloat16), 0, 25, METRICS["euclidean"])
+    assert st.q.stride(0) == 256
+    oi, osc = st.run()
+    torch.cuda.synchronize()
+    assert np.array_equal(oi.cpu().numpy().view(np.uint32), i1)
+    assert np.array_equal(osc.cpu().numpy().astype(np.float64), s1)
