@@ -80,6 +80,27 @@ def cpu_baseline(q_dev, c_dev, k, metric, n_sample, threads):
     return n_sample / dt, dt
 
 
+def numpy_comparator_qps(q_dev, c_dev, k, n_sample):
+    """SURVEY 8d CPU baseline (2): the README's NumPy comparator
+    (examples/benchmark_topk.py:14-33 in the reference) restated -- L2-normalise
+    both sides, one BLAS GEMM, a per-row partial selection of k, then a sort
+    of those k -- on the first n_sample queries against the full corpus.
+    Cosine only; BLAS threads as the environment sets them."""
+    q = q_dev[:n_sample].float().cpu().numpy()
+    c = c_dev.float().cpu().numpy()
+    t0 = time.perf_counter()
+    qn = q / np.sqrt((q * q).sum(axis=1, keepdims=True))
+    cn = c / np.sqrt((c * c).sum(axis=1, keepdims=True))
+    sim = qn @ cn.T
+    cut = sim.shape[1] - k
+    part = np.argpartition(sim, cut, axis=1)[:, cut:]
+    vals = np.take_along_axis(sim, part, axis=1)
+    order = np.argsort(-vals, axis=1)
+    np.take_along_axis(part, order, axis=1)
+    dt = time.perf_counter() - t0
+    return n_sample / dt, dt
+
+
 def boundary_rates(q_dev, c_dev, k, metric_id, compute=0):
     """Host-boundary rates: host f32 buffers in, host idx/score
     out, through the C ABI, one call each (untimed by the contract's clock):
@@ -166,7 +187,7 @@ def main():
                     help="queries timed on the CPU baseline vs the full corpus (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
-    ap.add_argument("--extra", default="c4",
+    ap.add_argument("--extra", default="c4,c1,c2",
                     help="comma-separated secondary configs measured after the main line (N=1; '' = none)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 torch top-k")
     args = ap.parse_args()
@@ -312,6 +333,17 @@ def main():
             "sample": f"first {n_s} queries x full {N}-row corpus, {D}d {cdt} {metric} k={k}; "
                       f"oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select), {cpu_dt:.1f}s",
         }
+    cpu_np = None
+    if args.cpu_sample and world == 1 and metric == "cosine":
+        n_s = min(args.cpu_sample, M)
+        np_qps, np_dt = numpy_comparator_qps(q, c, k, n_s)
+        cpu_np = {
+            "value": round(np_qps, 2), "unit": "queries/s",
+            "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+            "kind": "port",
+            "sample": f"first {n_s} queries x full {N}-row corpus; the reference README's NumPy "
+                      f"comparator (normalise, BLAS GEMM, argpartition, argsort), {np_dt:.1f}s",
+        }
     line = {
         "metric": "cosine top-k queries/sec",
         "value": round(qps, 2),
@@ -331,6 +363,7 @@ def main():
                    "parallelism": f"corpus-row-shard x{world}" if world > 1 else "single GPU"},
         "roofline": roofline,
         "cpu_baseline": cpu,
+        "cpu_baseline_numpy": cpu_np,
         "boundary": boundary,
         "extra": extra,
         "check": check,
