@@ -200,13 +200,17 @@ void plan_units(int64_t m, int64_t n, int bm, int bn, int cus, double unit_overh
 // Tile-shape variant: PMM_GEMM_VARIANT overrides; otherwise the preferred
 // order below, skipping variants whose LDS (staging + per-wave scratch) does
 // not fit in the CU's 160 KiB.
-int choose_variant(int mode, int capg) {
+// Small problems (fewer than 4 x CUs 256 x 256 tiles: the reference's own
+// 1000 x 10000 benchmark size) fill the chip better with 128 x 128 tiles.
+int choose_variant(int mode, int capg, int64_t m = 1 << 30, int64_t n = 1 << 30, int cus = 256) {
   static int env = -2;
   if (env == -2) {
     const char *e = getenv("PMM_GEMM_VARIANT");
     env = e ? atoi(e) : -1;
   }
   if (env >= 0 && env < 4 && gemm_f32_lds_bytes(env, mode, capg) <= 160 * 1024) return env;
+  if (cdiv(m, 256) * cdiv(n, 256) < 4 * (int64_t)cus && gemm_f32_lds_bytes(0, mode, capg) <= 160 * 1024)
+    return 0;
   // measured on c3 (100k x 1M x 768 cosine k=100): v3 136.9, v2 133.1, v1 120.5 TFLOP/s
   static const int order[4] = {3, 2, 0, 1};
   for (int v : order)
@@ -220,7 +224,7 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
               int compute = PMM_COMPUTE_F32) {
   p.capg = next_pow2((int)k + 64, 128);
   const bool bf16 = compute == PMM_COMPUTE_BF16;
-  p.variant = bf16 ? -1 : choose_variant(0, p.capg);
+  p.variant = bf16 ? -1 : choose_variant(0, p.capg, m, n, cus);
   const int bm = bf16 ? kBf16BM : gemm_f32_bm(p.variant);
   const int bn = bf16 ? kBf16BN : gemm_f32_bn(p.variant);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
@@ -278,6 +282,24 @@ void plan_materialise(int64_t m, int64_t n, int64_t k, size_t elem, MatPlan &p) 
   p.total = off;
 }
 
+// Page-locks a caller's host output buffer for the duration of a call so the
+// D2H copy of an m x n result runs at full link rate instead of through the
+// runtime's pageable staging (PMM_PIN_OUTPUT=0 disables; a failed
+// registration just leaves the copy pageable).
+struct HostPin {
+  void *p = nullptr;
+  HostPin(void *ptr, size_t bytes) {
+    static const bool on = !(getenv("PMM_PIN_OUTPUT") && atoi(getenv("PMM_PIN_OUTPUT")) == 0);
+    if (on && bytes >= (size_t(8) << 20) && hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess)
+      p = ptr;
+    else
+      (void)hipGetLastError();
+  }
+  ~HostPin() {
+    if (p) (void)hipHostUnregister(p);
+  }
+};
+
 int check_metric(int metric) {
   if (metric != kMetricCosine && metric != kMetricDot && metric != kMetricEuclidean)
     return fail(PMM_ERR_ARG, "invalid metric id %d", metric);
@@ -289,7 +311,7 @@ int gemm_store_f32(const float *q, int64_t ldq, int64_t rows, const float *c, in
                    int64_t d, int metric, int store_metric, const float *qn, const float *cn,
                    float *out, int64_t ldo, unsigned *counter, int cus, hipStream_t s) {
   Plan p;
-  p.variant = choose_variant(1, 0);
+  p.variant = choose_variant(1, 0, rows, n, cus);
   plan_units(rows, n, gemm_f32_bm(p.variant), gemm_f32_bn(p.variant), cus, 0.1, 1 << 20, p);
   GemmF32Args a{};
   a.q = q;
@@ -866,6 +888,7 @@ int pmm_matmul_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t
   if ((rc = upload_padded(b + off_c, c, n, d, dp, 4, s))) return rc;
   const float *dq = (const float *)(b + off_q), *dc = (const float *)(b + off_c);
   float *dout = (float *)(b + off_o);
+  HostPin pin(out, (size_t)m * n * 4);
   for (int64_t r0 = 0; r0 < m; r0 += rows_chunk) {
     const int64_t rows = std::min<int64_t>(rows_chunk, m - r0);
     rc = gemm_store_f32(dq + r0 * dp, dp, rows, dc, dp, n, dp, kMetricDot, 0, nullptr, nullptr,
@@ -897,6 +920,7 @@ int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64
   if ((rc = upload_padded(b + off_c, c, n, d, dp, 8, s))) return rc;
   const double *dq = (const double *)(b + off_q), *dc = (const double *)(b + off_c);
   double *dout = (double *)(b + off_o);
+  HostPin pin(out, (size_t)m * n * 8);
   for (int64_t r0 = 0; r0 < m; r0 += rows_chunk) {
     const int64_t rows = std::min<int64_t>(rows_chunk, m - r0);
     {
