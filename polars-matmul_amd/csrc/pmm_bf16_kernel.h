@@ -170,7 +170,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // holds (a unit's first tiles) takes the per-score path through a global
 // queue instead.
 // ===========================================================================
-template <int KS, int METRIC, int NST>  // KS = padded D / 128; NST = ring slots (3 or 4)
+// KS = padded D / 128; NST = ring slots; PF = fragment prefetch depth (substeps)
+template <int KS, int METRIC, int NST, int PF>
 __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u64 *thr_l = (u64 *)(smem + OFF_THR);
@@ -195,6 +196,12 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
   float *sbuf = (float *)(smem + OFF_STAGE) + ((size_t)wid * 64 + lane) * 16;
   constexpr bool XFORM = (METRIC != kMetricDot);
   constexpr int G = KS * KSUB;  // MFMA substeps per tile
+  // PIPE: compute tile t-1's survivor bits between tile t's MFMAs (two
+  // accumulator sets; the asm pins keep LLVM from sinking the work below
+  // the loop).  Measured no faster than computing them right after each
+  // tile's own K-loop (the loop grew by what the epilogue lost), so it is
+  // off and the kernel runs one accumulator set.
+  constexpr bool PIPE = false;
 
   // Loop-invariant per-lane byte offsets of this wave's corpus DMA pieces:
   // piece i = 4 corpus rows x 256 B; 16-byte chunk c of row r lands in LDS
@@ -426,7 +433,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
       const uint64_t tts = timing ? __builtin_amdgcn_s_memtime() : 0;
       const int pt = tile - 1;
       float cv[NB], nlo[16];
-      tile_consts(pt, cv, nlo);  // (garbage for a unit's first tile: unused)
+      if (PIPE) tile_consts(pt, cv, nlo);  // (garbage for a unit's first tile: unused)
       uint32_t bits[NB];
 #pragma unroll
       for (int c = 0; c < NB; c++) bits[c] = 0u;
@@ -449,17 +456,21 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const char *st = ring + sl * STAGE;
-        bf16x8 bq[2][NB];
+        // corpus fragments read PF substeps ahead of their MFMAs
+        bf16x8 bq[PF + 1][NB];
 #pragma unroll
-        for (int c = 0; c < NB; c++)
-          bq[0][c] = *(const bf16x8 *)(st + b_rd + c * 32 * KB + 16 * ((8 * h) ^ swz));
+        for (int p = 0; p < PF; p++)
+#pragma unroll
+          for (int c = 0; c < NB; c++)
+            bq[p][c] = *(const bf16x8 *)(st + b_rd + c * 32 * KB + 16 * ((8 * h + p) ^ swz));
 #pragma unroll
         for (int sub = 0; sub < KSUB; sub++) {
-          const int cur = sub & 1;
-          if (sub + 1 < KSUB) {
-            const int co = 16 * ((8 * h + sub + 1) ^ swz);
+          const int cur = sub % (PF + 1);
+          if (sub + PF < KSUB) {
+            const int co = 16 * ((8 * h + sub + PF) ^ swz);
 #pragma unroll
-            for (int c = 0; c < NB; c++) bq[cur ^ 1][c] = *(const bf16x8 *)(st + b_rd + c * 32 * KB + co);
+            for (int c = 0; c < NB; c++)
+              bq[(sub + PF) % (PF + 1)][c] = *(const bf16x8 *)(st + b_rd + c * 32 * KB + co);
           }
 #pragma unroll
           for (int c = 0; c < NB; c++) {
@@ -478,7 +489,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
             stage(slj, rsrc_b(tile + adv), (ks + jj) % KS, tile + adv);
           }
           // this substep's share of the previous tile's survivor test
-          {
+          if constexpr (PIPE) {
             const int gidx = ks * KSUB + sub;
 #pragma unroll
             for (int pidx = 0; pidx < 64; pidx++) {
@@ -486,6 +497,9 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
               const int c = pidx >> 4, e = pidx & 15;
               const float d = prefilter_diff<METRIC>(pv[c][e], cv[c], nlo[e]);
               bits[c] = (bits[c] << 1) | (uint32_t)!(d < 0.0f);
+              // opaque use in place: without it LLVM sinks this loop-invariant
+              // work below the K-loop (sched_barrier acts too late to stop it)
+              asm volatile("" : "+v"(bits[c]));
             }
           }
           __builtin_amdgcn_sched_barrier(0);
@@ -495,7 +509,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
       mfma_drain(acc);
       const uint64_t tte = timing ? __builtin_amdgcn_s_memtime() : 0;
       if (timing) cy_loop += tte - tts;
-      if (has_prev && a.ablate != 1) extract(pv, pt, bits);
+      if (PIPE && has_prev && a.ablate != 1) extract(pv, pt, bits);
       if (timing) cy_ext += __builtin_amdgcn_s_memtime() - tte;
     };
 
@@ -516,16 +530,28 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
       extract(pv, pt, bits);
     };
 
-    f32x16 accA[NB], accB[NB];
+    if constexpr (PIPE) {
+      f32x16 accA[NB], accB[NB];
 #pragma unroll
-    for (int c = 0; c < NB; c++) accB[c] = (f32x16){};
-    for (int tile = t0; tile < t1; tile += 2) {
-      tile_step(accA, accB, tile, tile > t0);
-      if (tile + 1 < t1) tile_step(accB, accA, tile + 1, true);
-    }
-    if (a.ablate != 1) {
-      if (((t1 - 1 - t0) & 1) == 0) tile_last(accA, t1 - 1);
-      else tile_last(accB, t1 - 1);
+      for (int c = 0; c < NB; c++) accB[c] = (f32x16){};
+      for (int tile = t0; tile < t1; tile += 2) {
+        tile_step(accA, accB, tile, tile > t0);
+        if (tile + 1 < t1) tile_step(accB, accA, tile + 1, true);
+      }
+      if (a.ablate != 1) {
+        if (((t1 - 1 - t0) & 1) == 0) tile_last(accA, t1 - 1);
+        else tile_last(accB, t1 - 1);
+      }
+    } else {
+      f32x16 acc[NB];
+      for (int tile = t0; tile < t1; tile++) {
+        tile_step(acc, acc, tile, false);
+        if (a.ablate != 1) {
+          const uint64_t tx = timing ? __builtin_amdgcn_s_memtime() : 0;
+          tile_last(acc, tile);
+          if (timing) cy_ext += __builtin_amdgcn_s_memtime() - tx;
+        }
+      }
     }
     // the K-steps issued past the unit's last tile land before the ring is
     // reused by the next unit
@@ -545,22 +571,24 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
   }
 }
 
-template <int KS, int METRIC, int NST>
+template <int KS, int METRIC, int NST, int PF>
 static hipError_t launch_bf16_n(const GemmF32Args &a, int grid, size_t lds, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)gemm_bf16_kernel<KS, METRIC, NST>,
+    hipError_t e = hipFuncSetAttribute((const void *)gemm_bf16_kernel<KS, METRIC, NST, PF>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  gemm_bf16_kernel<KS, METRIC, NST><<<dim3(grid), dim3(NW * 64), lds, s>>>(a);
+  gemm_bf16_kernel<KS, METRIC, NST, PF><<<dim3(grid), dim3(NW * 64), lds, s>>>(a);
   return hipGetLastError();
 }
 template <int KS, int METRIC>
 static hipError_t launch_bf16_t(const GemmF32Args &a, int grid, size_t lds, hipStream_t s) {
   // three ring slots: a fourth (measured at D = 768) gained nothing
-  return launch_bf16_n<KS, METRIC, 3>(a, grid, lds, s);
+  // fragment prefetch one substep ahead: two (measured on the same box) was
+  // 0.6% slower
+  return launch_bf16_n<KS, METRIC, 3, 1>(a, grid, lds, s);
 }
 
 template <int KS>

@@ -45,6 +45,7 @@ struct GemmF32Args {
   int nst;                        // bf16 kernel: LDS ring slots (3 or 4)
   int round_sync;                 // bf16 kernel: align workgroups at unit rounds (speed only)
   int sync_timeout;               // bf16 kernel: round-barrier spin limit (100 MHz ticks)
+  int pf;                         // bf16 kernel: corpus-fragment prefetch depth (1 or 2 substeps)
   unsigned long long *stats;      // PMM_STATS only: [queued, flagged groups, tiles, compactions]
 };
 
