@@ -188,7 +188,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
     ap.add_argument("--extra", default="c4,c1,c2",
-                    help="comma-separated secondary configs measured after the main line (N=1; '' = none)")
+                    help="comma-separated secondary configs measured after the main line (N=1; 'none' = none)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 torch top-k")
     args = ap.parse_args()
 
@@ -292,7 +292,7 @@ def main():
         del runner, ws
         torch.cuda.empty_cache()
         extra = {}
-        for name in [x for x in args.extra.split(",") if x and x != args.config]:
+        for name in [x for x in args.extra.split(",") if x and x not in (args.config, "none")]:
             extra[name] = measure_extra(name, args.steps, args.warmup, dev)
             log(f"extra {name}: {extra[name]}")
 
