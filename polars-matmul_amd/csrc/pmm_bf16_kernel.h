@@ -47,8 +47,7 @@ constexpr int OFF_CNT = OFF_THR + BM * 8;
 constexpr int OFF_QEX = OFF_CNT + BM * 4;
 constexpr int OFF_LO = OFF_QEX + BM * 4;
 constexpr int OFF_CV = OFF_LO + BM * 4;      // pre-filter column factors, 4 tiles
-constexpr int OFF_CN = OFF_CV + 4 * BN * 4;  // exact column norms (pass 2), 4 tiles
-constexpr int OFF_QUEUE = OFF_CN + 4 * BN * 4;
+constexpr int OFF_QUEUE = OFF_CV + 4 * BN * 4;
 constexpr int OFF_STAGE = OFF_QUEUE + NW * QCAP * 8;  // survivor staging [wave][lane][16]
 constexpr int OFF_UNIT = OFF_STAGE + NW * 64 * 16 * 4;
 constexpr int OFF_RING = (OFF_UNIT + 16 + 255) & ~255;
@@ -179,7 +178,6 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
   float *qex_l = (float *)(smem + OFF_QEX);
   float *lo_l = (float *)(smem + OFF_LO);
   float *cv_l = (float *)(smem + OFF_CV);
-  float *cn_l = (float *)(smem + OFF_CN);
   int *unit_l = (int *)(smem + OFF_UNIT);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -216,7 +214,6 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
   }
   const int swz = r32 & 15;
   const int b_rd = r32 * KB;
-  const uint32_t lane_hi0 = 4u * (uint32_t)h + ((uint32_t)r32 << 5);
 
   uint32_t st_q = 0, st_g = 0, st_c = 0;  // PMM_STATS counters (wave-uniform)
   uint64_t cy_loop = 0, cy_ext = 0, cy_drain = 0;  // PMM_STATS: shader cycles per phase
@@ -302,7 +299,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
       return make_rsrc(a.cb + (int64_t)col0 * a.ldc, (int64_t)max(0, min(BN, a.N - col0)) * a.ldc * 2);
     };
     // one K-step's DMA: this wave's BPIECES pieces, plus (on a tile's first
-    // step) its share of the tile's pre-filter factors and exact norms
+    // step) its share of the tile's pre-filter factors
     auto stage = [&](int slot, __amdgpu_buffer_rsrc_t rb, int ks, int tile) {
       char *st = ring + slot * STAGE;
       const uint32_t soff = (uint32_t)ks * (uint32_t)KB;
@@ -314,16 +311,12 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
         const int col0 = tile * BN + wid * CV_PER_WAVE;
         const int64_t nb = (int64_t)max(0, min(CV_PER_WAVE, a.N - col0)) * 4;
         const __amdgpu_buffer_rsrc_t rc = make_rsrc(a.cpre + col0, nb);
-        const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.cn + col0, nb);
         const int o = (tile & 3) * BN + wid * CV_PER_WAVE;
         // lanes past CV_PER_WAVE stay masked (an LDS-DMA writes one dword per
         // ACTIVE lane); vmcnt still counts one instruction per wave
-        if (lane < CV_PER_WAVE) {
+        if (lane < CV_PER_WAVE)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (LDS_AS void *)(cv_l + o), 4,
                                                    (uint32_t)(lane * 4), 0, 0, 0);
-          __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (LDS_AS void *)(cn_l + o), 4,
-                                                   (uint32_t)(lane * 4), 0, 0, 0);
-        }
       }
     };
 
@@ -331,23 +324,31 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
     for (int j = 0; j < nst - 1; j++) stage(j, rsrc_b(t0 + j / KS), j % KS, t0 + j / KS);
     int sl = 0;  // ring slot of the current K-step
 
-    // ---- pass 2: exact re-score of the LDS-queued survivors of tile pt ----
-    auto drain = [&](int qlen, int pt) {
+    // ---- pass 2: exact re-score of the LDS-queued survivors ----
+    // Deferred: the queue (item = accumulator bits | (row-in-wave | global
+    // column << 5) << 32) collects survivors across tiles and drains only when
+    // it could overflow or at the unit's end, in full 64-item rounds; the
+    // exact column norms come from global memory, one load per item.
+    int qlen = 0;  // this wave's queued items (wave-uniform)
+    auto drain = [&]() {
       st_q += (uint32_t)qlen;
-      if (a.ablate == 2 || qlen == 0) return;
+      if (a.ablate == 2 || qlen == 0) {
+        qlen = 0;
+        return;
+      }
       const uint64_t tdr = timing ? __builtin_amdgcn_s_memtime() : 0;
-      const int col0 = pt * BN;
+      wave_sync();
       for (int base = 0; base < qlen; base += 64) {
         const int i = base + lane;
         if (i < qlen) {
           const u64 it = lq[i];
           const float v = __uint_as_float((uint32_t)it);
           const int rl = (int)((it >> 32) & 31u);
-          const int cl = (int)(it >> 37);
-          const float sc = exact_score<METRIC>(v, XFORM ? qex_w[rl] : 0.0f,
-                                               XFORM ? cn_l[(pt & 3) * BN + cl] : 0.0f);
+          const int gcol = (int)(it >> 37);
+          const float sc =
+              exact_score<METRIC>(v, XFORM ? qex_w[rl] : 0.0f, XFORM ? a.cn[gcol] : 0.0f);
           const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
-          const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)(col0 + cl));
+          const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
           if (comp > thr_w[rl]) {
             const unsigned pos = atomicAdd(&cnt_w[rl], 1u);
             a.cand[((int64_t)(wrow0 + rl) * a.S + s) * a.capg + pos] = comp;
@@ -369,6 +370,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
           wave_sync();
         }
       }
+      qlen = 0;
       if (timing) cy_drain += __builtin_amdgcn_s_memtime() - tdr;
     };
 
@@ -381,7 +383,6 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
     // overflow (a unit's first tiles).
     auto extract = [&](const f32x16 (&pv)[NB], int pt, uint32_t (&bits)[NB])
         __attribute__((always_inline)) {
-      int qlen = 0;
 #pragma unroll
       for (int c = 0; c < NB; c++) {
         uint32_t b = (pt * BN + 32 * c + r32 < a.N) ? bits[c] : 0u;  // columns past N
@@ -401,22 +402,17 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
             b &= ~(1u << j);
             const int e = 15 - j;
             const float v = sbuf[e];
-            const uint32_t hi = lane_hi0 + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
+            const uint32_t hi = (uint32_t)(4 * h + (e & 3) + 8 * (e >> 2)) |
+                                ((uint32_t)(pt * BN + 32 * c + r32) << 5);
             lq[qlen + lanes_below(m)] = (u64)__float_as_uint(v) | ((u64)hi << 32);
           } else if (act) {
             b &= b - 1u;
           }
           qlen += __popcll(m);
-          if (qlen > QCAP - 64) {
-            wave_sync();
-            drain(qlen, pt);
-            qlen = 0;
-          }
+          if (qlen > QCAP - 64) drain();
         }
       }
       st_g++;
-      wave_sync();
-      drain(qlen, pt);
     };
 
     auto tile_consts = [&](int pt, float (&cv)[NB], float (&nlo)[16]) __attribute__((always_inline)) {
@@ -440,17 +436,17 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
 #pragma unroll
       for (int ks = 0; ks < KS; ks++) {
         // step (tile, ks) landed: only the DMAs of the nst - 2 younger steps
-        // may still be in flight (a step's count: BPIECES, +2 on a tile's
-        // first step for the factors and norms); ks is a constant after
+        // may still be in flight (a step's count: BPIECES, +1 on a tile's
+        // first step for the pre-filter factors); ks is a constant after
         // unrolling, so the branches fold away
-        const int x1 = (XFORM && (ks + 1) % KS == 0) ? 2 : 0;
-        const int x2 = (XFORM && (ks + 2) % KS == 0) ? 2 : 0;
+        const int x1 = (XFORM && (ks + 1) % KS == 0) ? 1 : 0;
+        const int x2 = (XFORM && (ks + 2) % KS == 0) ? 1 : 0;
         if (nst == 4) {
-          if (x1 + x2 == 4) wait_vm<2 * BPIECES + 4>();
-          else if (x1 + x2 == 2) wait_vm<2 * BPIECES + 2>();
+          if (x1 + x2 == 2) wait_vm<2 * BPIECES + 2>();
+          else if (x1 + x2 == 1) wait_vm<2 * BPIECES + 1>();
           else wait_vm<2 * BPIECES>();
         } else {
-          if (x1) wait_vm<BPIECES + 2>();
+          if (x1) wait_vm<BPIECES + 1>();
           else wait_vm<BPIECES>();
         }
         __builtin_amdgcn_s_barrier();
@@ -553,6 +549,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
         }
       }
     }
+    drain();  // the unit's remaining survivors
     // the K-steps issued past the unit's last tile land before the ring is
     // reused by the next unit
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -470,10 +470,13 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
 
 // bf16 compute path over device bf16 rows (row strides ldq / ldc >=
 // roundup(d, 128), zero-padded); d is the logical dimension.
-int bf16_limits(int64_t d, int64_t k) {
+int bf16_limits(int64_t d, int64_t k, int64_t n) {
   if (cdiv(d, kBf16DAlign) * kBf16DAlign > kBf16MaxD)
     return fail(PMM_ERR_UNSUPPORTED, "bf16 compute supports d <= %d (got %lld)", kBf16MaxD,
                 (long long)d);
+  if (n >= (int64_t(1) << 27))
+    return fail(PMM_ERR_UNSUPPORTED, "bf16 compute supports n < 2^27 corpus rows (got %lld)",
+                (long long)n);
   if (next_pow2((int)std::min<int64_t>(k, 1 << 20) + 64, 128) > kBf16MaxCapg)
     return fail(PMM_ERR_UNSUPPORTED, "bf16 compute supports k <= %d (got %lld)", kBf16MaxCapg - 64,
                 (long long)k);
@@ -726,7 +729,7 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
-  if (compute == PMM_COMPUTE_BF16 && (rc = bf16_limits(d, k))) return rc;
+  if (compute == PMM_COMPUTE_BF16 && (rc = bf16_limits(d, k, n))) return rc;
   int dev;
   if ((rc = ensure_device(&dev))) return rc;
   hipStream_t s;
@@ -784,7 +787,7 @@ int pmm_topk_bf16_device(const uint16_t *q, int64_t ldq, int64_t m, const uint16
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
-  if ((rc = bf16_limits(d, k))) return rc;
+  if ((rc = bf16_limits(d, k, n))) return rc;
   const int64_t dp = cdiv(d, kBf16DAlign) * kBf16DAlign;
   if (ldq % 8 != 0 || ldc % 8 != 0 || ldq < dp || ldc < dp || ((uintptr_t)q & 15) ||
       ((uintptr_t)c & 15))
