@@ -169,8 +169,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // holds (a unit's first tiles) takes the per-score path through a global
 // queue instead.
 // ===========================================================================
-// KS = padded D / 128; NST = ring slots; PF = fragment prefetch depth (substeps)
-template <int KS, int METRIC, int NST, int PF>
+// KS = padded D / 128; NST = ring slots; PF = fragment prefetch depth (substeps);
+// DEF = hold each K-step's last MFMA group back to after the next barrier
+template <int KS, int METRIC, int NST, int PF, int DEF>
 __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u64 *thr_l = (u64 *)(smem + OFF_THR);
@@ -200,6 +201,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
   // tile's own K-loop (the loop grew by what the epilogue lost), so it is
   // off and the kernel runs one accumulator set.
   constexpr bool PIPE = false;
+  constexpr bool DEFER = DEF != 0;
 
   // Loop-invariant per-lane byte offsets of this wave's corpus DMA pieces:
   // piece i = 4 corpus rows x 256 B; 16-byte chunk c of row r lands in LDS
@@ -433,6 +435,8 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
       uint32_t bits[NB];
 #pragma unroll
       for (int c = 0; c < NB; c++) bits[c] = 0u;
+      constexpr int NBQ = PF + 2;
+      bf16x8 bq[NBQ][NB];
 #pragma unroll
       for (int ks = 0; ks < KS; ks++) {
         // step (tile, ks) landed: only the DMAs of the nst - 2 younger steps
@@ -452,26 +456,37 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         const char *st = ring + sl * STAGE;
-        // corpus fragments read PF substeps ahead of their MFMAs
-        bf16x8 bq[PF + 1][NB];
+        // corpus fragments read PF substeps ahead of their MFMAs, into a
+        // rotation of PF + 2 buffers indexed by the tile's substep number
 #pragma unroll
         for (int p = 0; p < PF; p++)
 #pragma unroll
           for (int c = 0; c < NB; c++)
-            bq[p][c] = *(const bf16x8 *)(st + b_rd + c * 32 * KB + 16 * ((8 * h + p) ^ swz));
+            bq[(KSUB * ks + p) % NBQ][c] =
+                *(const bf16x8 *)(st + b_rd + c * 32 * KB + 16 * ((8 * h + p) ^ swz));
+        // the previous step's last MFMA group, held back from before the
+        // barrier (its fragments are in registers): it covers the latency of
+        // the reads just issued instead of the MFMA pipe idling behind them
+        if (DEFER && ks > 0) {
+#pragma unroll
+          for (int c = 0; c < NB; c++)
+            mfma_acc(acc[c], af[KSUB * ks - 1], bq[(KSUB * ks - 1) % NBQ][c]);
+        }
 #pragma unroll
         for (int sub = 0; sub < KSUB; sub++) {
-          const int cur = sub % (PF + 1);
+          const int gs = KSUB * ks + sub;
           if (sub + PF < KSUB) {
             const int co = 16 * ((8 * h + sub + PF) ^ swz);
 #pragma unroll
             for (int c = 0; c < NB; c++)
-              bq[(sub + PF) % (PF + 1)][c] = *(const bf16x8 *)(st + b_rd + c * 32 * KB + co);
+              bq[(gs + PF) % NBQ][c] = *(const bf16x8 *)(st + b_rd + c * 32 * KB + co);
           }
+          if (!(DEFER && sub == KSUB - 1 && ks < KS - 1)) {
 #pragma unroll
-          for (int c = 0; c < NB; c++) {
-            if (ks == 0 && sub == 0) mfma_first(acc[c], af[0], bq[cur][c]);
-            else mfma_acc(acc[c], af[KSUB * ks + sub], bq[cur][c]);
+            for (int c = 0; c < NB; c++) {
+              if (gs == 0) mfma_first(acc[c], af[0], bq[0][c]);
+              else mfma_acc(acc[c], af[gs], bq[gs % NBQ][c]);
+            }
           }
           if (sub == 0) {
             // step + nst - 1 goes out behind the first MFMA group, in one
@@ -568,16 +583,16 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
   }
 }
 
-template <int KS, int METRIC, int NST, int PF>
+template <int KS, int METRIC, int NST, int PF, int DEF>
 static hipError_t launch_bf16_n(const GemmF32Args &a, int grid, size_t lds, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)gemm_bf16_kernel<KS, METRIC, NST, PF>,
+    hipError_t e = hipFuncSetAttribute((const void *)gemm_bf16_kernel<KS, METRIC, NST, PF, DEF>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  gemm_bf16_kernel<KS, METRIC, NST, PF><<<dim3(grid), dim3(NW * 64), lds, s>>>(a);
+  gemm_bf16_kernel<KS, METRIC, NST, PF, DEF><<<dim3(grid), dim3(NW * 64), lds, s>>>(a);
   return hipGetLastError();
 }
 template <int KS, int METRIC>
@@ -585,7 +600,8 @@ static hipError_t launch_bf16_t(const GemmF32Args &a, int grid, size_t lds, hipS
   // three ring slots: a fourth (measured at D = 768) gained nothing
   // fragment prefetch one substep ahead: two (measured on the same box) was
   // 0.6% slower
-  return launch_bf16_n<KS, METRIC, 3, 1>(a, grid, lds, s);
+  if (a.defer) return launch_bf16_n<KS, METRIC, 3, 1, 1>(a, grid, lds, s);
+  return launch_bf16_n<KS, METRIC, 3, 1, 0>(a, grid, lds, s);
 }
 
 template <int KS>

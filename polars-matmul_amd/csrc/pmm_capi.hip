@@ -537,6 +537,8 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
   {
     a.nst = 3;  // LDS ring slots of the bf16 kernel
     a.pf = 1;
+    static const int defer_env = getenv("PMM_BF16_DEFER") ? atoi(getenv("PMM_BF16_DEFER")) : 1;
+    a.defer = defer_env;
     static const int sync_env = getenv("PMM_BF16_SYNC") ? atoi(getenv("PMM_BF16_SYNC")) : 1;
     a.round_sync = sync_env;
     // round-barrier spin limit: workgroups of one round finish up to a few ms

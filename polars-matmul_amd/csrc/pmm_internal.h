@@ -46,6 +46,7 @@ struct GemmF32Args {
   int round_sync;                 // bf16 kernel: align workgroups at unit rounds (speed only)
   int sync_timeout;               // bf16 kernel: round-barrier spin limit (100 MHz ticks)
   int pf;                         // bf16 kernel: corpus-fragment prefetch depth (1 or 2 substeps)
+  int defer;                      // bf16 kernel: hold each K-step's last MFMA group past the barrier
   unsigned long long *stats;      // PMM_STATS only: [queued, flagged groups, tiles, compactions]
 };
 
