@@ -91,34 +91,6 @@ __device__ __forceinline__ void mfma_drain(f32x16 (&acc)[NBX]) {
   for (int c = 1; c < NBX - 1; c++) asm volatile("" : "+v"(acc[c]));
 }
 
-// Fast pre-filter of one 32-column group: d = (pre-filter value) - lo per
-// score (cosine: one FMA), NaN-propagating max over the lane's 16 rows.
-// d >= 0 iff the exact pre-filter value >= lo (a rounded difference keeps its
-// sign), so a group whose max is < 0 on every lane has no survivor.
-template <int METRIC>
-__device__ __forceinline__ float group_dmax(const f32x16 &v, float cv, const float (&lo)[16]) {
-  float dmax = 0.0f;
-#pragma unroll
-  for (int e = 0; e < 16; e++) {
-    float d;
-    if (METRIC == kMetricDot) d = v[e] - lo[e];
-    else if (METRIC == kMetricCosine) d = fmaf(v[e], cv, -lo[e]);
-    else d = fmaf(2.0f, v[e], -cv) - lo[e];
-    dmax = (e == 0) ? d : __builtin_elementwise_maximum(dmax, d);
-  }
-  return dmax;
-}
-
-// Pre-filter difference of one score: >= 0 (or NaN) iff the score may enter
-// the row's top-k (see prefilter_bound); a rounded difference keeps the sign
-// of the exact one.
-template <int METRIC>
-__device__ __forceinline__ float prefilter_diff(float v, float cv, float lo) {
-  if (METRIC == kMetricDot) return v - lo;
-  if (METRIC == kMetricCosine) return fmaf(v, cv, -lo);
-  return fmaf(2.0f, v, -cv) - lo;
-}
-
 // Wave-wide OR / sum in DPP steps (quad perms, row half-mirror, row mirror,
 // row_bcast:15, row_bcast:31), a few cycles each, instead of ds_bpermute
 // shuffles (an LDS round trip each); the result is uniform (lane 63's).

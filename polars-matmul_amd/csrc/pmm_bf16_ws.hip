@@ -1,0 +1,47 @@
+// pmm_bf16_ws.hip -- host side of the wave-specialised bf16 kernel
+// (pmm_bf16_ws_kernel.h; per-D instantiations in pmm_bf16_ws_ks.hip).
+#include "pmm_bf16_ws_kernel.h"
+
+#include <hip/hip_runtime.h>
+
+namespace pmm {
+
+size_t gemm_bf16_ws_lds_bytes(int capg, int D) {
+  size_t scr = 0;
+  switch (D / 128) {
+    case 1: scr = ws::Carve<1>::OFF_SCR; break;
+    case 2: scr = ws::Carve<2>::OFF_SCR; break;
+    case 3: scr = ws::Carve<3>::OFF_SCR; break;
+    case 4: scr = ws::Carve<4>::OFF_SCR; break;
+    case 5: scr = ws::Carve<5>::OFF_SCR; break;
+    default: scr = ws::Carve<6>::OFF_SCR; break;
+  }
+  return scr + (size_t)ws::NWE * capg * 8;
+}
+
+hipError_t launch_bf16_ws_ks1(const GemmF32Args &a, int grid, size_t lds, hipStream_t s);
+hipError_t launch_bf16_ws_ks2(const GemmF32Args &a, int grid, size_t lds, hipStream_t s);
+hipError_t launch_bf16_ws_ks3(const GemmF32Args &a, int grid, size_t lds, hipStream_t s);
+hipError_t launch_bf16_ws_ks4(const GemmF32Args &a, int grid, size_t lds, hipStream_t s);
+hipError_t launch_bf16_ws_ks5(const GemmF32Args &a, int grid, size_t lds, hipStream_t s);
+hipError_t launch_bf16_ws_ks6(const GemmF32Args &a, int grid, size_t lds, hipStream_t s);
+
+hipError_t launch_gemm_bf16_ws(const GemmF32Args &a, int grid, hipStream_t s) {
+  const size_t lds = gemm_bf16_ws_lds_bytes(a.capg, a.D);
+  // the kernel's grid and tile shapes assume: whole 128-wide K-steps, a
+  // capacity the LDS carve holds, and every unit's tiles inside the corpus
+  if (lds > 160 * 1024 || a.D % kBf16DAlign != 0 || a.capg > kBf16WsMaxCapg || a.tps < 1 ||
+      (int64_t)a.ntiles * ws::BN < a.N || (int64_t)a.QB * ws::BM < a.M)
+    return hipErrorInvalidValue;
+  switch (a.D / 128) {
+    case 1: return launch_bf16_ws_ks1(a, grid, lds, s);
+    case 2: return launch_bf16_ws_ks2(a, grid, lds, s);
+    case 3: return launch_bf16_ws_ks3(a, grid, lds, s);
+    case 4: return launch_bf16_ws_ks4(a, grid, lds, s);
+    case 5: return launch_bf16_ws_ks5(a, grid, lds, s);
+    case 6: return launch_bf16_ws_ks6(a, grid, lds, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+}  // namespace pmm

@@ -1,0 +1,600 @@
+// pmm_bf16_ws_kernel.h -- wave-specialised bf16 fused GEMM + top-k kernel
+// (PMM_COMPUTE_BF16; BASELINE configs[3]: 100k x 1M x 768 bf16 cosine k=100).
+// Instantiated per padded-D step count by pmm_bf16_ks.hip; host side in
+// pmm_bf16.hip.  Same arithmetic and results as pmm_bf16_kernel.h (bf16
+// operands, f32 accumulation on v_mfma_f32_32x32x16_bf16, the f32 path's
+// metric epilogue, pre-filter, candidate buffers and merge).
+//
+// Why a second bf16 kernel: at one wave per SIMD (pmm_bf16_kernel.h) every
+// latency of the top-k epilogue (LDS round trips, the survivors' exact
+// re-score, candidate stores, compactions) stalls the matrix pipe: measured
+// at 100k x 1M x 768 the epilogue adds 50% to the K-loop's time.  Here the
+// work is split by role, two waves per SIMD:
+//
+//   * 4 MFMA waves (one per SIMD).  Wave w keeps its 32 query rows x D in
+//     AGPRs for a whole work unit (192 registers at D = 768) and streams the
+//     corpus: per 64-column tile, KS K-steps of 128 bf16, each 8 substeps of
+//     two v_mfma_f32_32x32x16_bf16 with the corpus fragments read from LDS
+//     one substep ahead.  After a tile's K-loop it hands its 32 x 64 f32
+//     accumulators to LDS (8 ds_write_b128) and starts the next tile.
+//     No global memory traffic and no epilogue in this role.
+//   * 4 epilogue waves (one per SIMD).  Wave 4 + w owns wave w's 32 rows:
+//     their top-k state (threshold, candidate counts, LDS) has one owner.
+//     It issues the corpus LDS-DMA for the ring (taking the DMA issue cost off
+//     the MFMA waves) and, while the MFMA waves compute tile t, runs the
+//     pre-filter, the exact re-score of the survivors, the candidate appends
+//     and compactions of tile t - 1.
+//
+// Synchronisation: every wave of the workgroup executes the same number of
+// s_barriers (the two roles run separate loops with equal trip counts; the
+// per-unit barriers are outside the role branches).  Barrier B_g opens corpus
+// K-step g (ring slot g % NST): before it the epilogue waves have waited
+// (counted vmcnt) for step g's DMA, and the MFMA waves have retired their
+// LDS reads of step g - 1 (lgkmcnt(0)), so after it step g + NST - 1 may be
+// DMA'd into step g - 1's slot.  A tile's accumulators are written before
+// the barrier opening the next tile and read by the epilogue waves after it
+// (double-buffered: tile t + 2 reuses tile t's buffer, written after the
+// epilogue waves have passed the barriers of tile t + 1, by which point they
+// finished with tile t).  The pre-filter column factors and column norms of a
+// tile ride with the tile's first K-step into an 8-tile LDS ring.
+#pragma once
+#include "pmm_device.h"
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pmm {
+
+namespace ws {
+typedef __attribute__((__vector_size__(8 * sizeof(__bf16)))) __bf16 bf16x8;
+
+constexpr int NWM = 4;                       // MFMA waves (1 per SIMD)
+constexpr int NWE = 4;                       // epilogue waves (1 per SIMD)
+constexpr int NTH = (NWM + NWE) * 64;
+constexpr int BM = 32 * NWM;                 // query rows per workgroup
+constexpr int BN = kBf16WsBN;                // corpus columns per tile
+constexpr int NB = BN / 32;                  // 32x32 accumulators per MFMA wave
+constexpr int KB = 256;                      // bytes of a row per K-step (128 bf16)
+constexpr int KSUB = KB / 32;                // MFMA substeps (K = 16) per K-step
+constexpr int PF = 2;                        // corpus fragments read PF substeps ahead
+constexpr int STAGE = BN * KB;               // one K-step of one tile
+constexpr int P = STAGE / 1024 / NWE;        // 1 KiB DMA pieces per epilogue wave per step
+constexpr int CVT = 8;                       // tiles in the column-factor ring
+constexpr int HAND = 32 * BN * 4;            // accumulator hand-off per wave per tile
+// LDS carve
+constexpr int OFF_THR = 0;
+constexpr int OFF_CNT = OFF_THR + BM * 8;
+constexpr int OFF_QEX = OFF_CNT + BM * 4;
+constexpr int OFF_LO = OFF_QEX + BM * 4;
+constexpr int OFF_UNIT = OFF_LO + BM * 4;
+constexpr int OFF_CVR = (OFF_UNIT + 16 + 255) & ~255;   // pre-filter factors [CVT][BN]
+constexpr int OFF_CNR = OFF_CVR + CVT * BN * 4;          // column norms [CVT][BN]
+constexpr int OFF_HAND = (OFF_CNR + CVT * BN * 4 + 255) & ~255;  // [NHB][NWM][HAND]
+constexpr int QCAP = 256;                    // survivor queue per epilogue wave
+// The rest of the carve depends on the K-steps per tile.  With KS >= 3 the
+// epilogue waves are done with tile t's accumulators (read in the first two
+// intervals of tile t + 1) before the MFMA waves write tile t + 1's (after
+// the last barrier of tile t + 1), so one hand-off buffer suffices and its
+// 32 KiB go to the corpus ring: 6 slots = 4 K-steps (64 KiB) in flight per
+// CU, which the L2 / MALL latency needs at ~55 GB/s per CU.
+template <int KS>
+struct Carve {
+  static constexpr int NHB = KS >= 3 ? 1 : 2;              // hand-off buffers
+  static constexpr int NST = KS >= 3 ? 6 : 4;              // corpus ring slots
+  static constexpr int OFF_RING = OFF_HAND + NHB * NWM * HAND;
+  static constexpr int OFF_QUEUE = OFF_RING + NST * STAGE;  // [NWE][QCAP] u64
+  static constexpr int OFF_SCR = OFF_QUEUE + NWE * QCAP * 8;  // [NWE][capg] compaction scratch
+  static_assert(OFF_RING % 256 == 0 && STAGE % 1024 == 0, "LDS carve alignment");
+};
+static_assert(P * NWE * 1024 == STAGE, "a K-step splits into whole 1 KiB pieces per wave");
+static_assert(BN / NWE <= 64, "one column-factor DMA per epilogue wave covers its share");
+
+// DMA instructions an epilogue wave issues for one K-step (corpus pieces, plus
+// the pre-filter factors and norms of the tile on its first step)
+template <bool XFORM>
+constexpr int step_dmas(int ks) { return P + ((XFORM && ks == 0) ? 2 : 0); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// the same with a count that is constant after unrolling (folds to one wait)
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+#define PMM_WCASE(N) \
+  case N: wait_vm<N>(); break;
+    PMM_WCASE(2) PMM_WCASE(4) PMM_WCASE(6) PMM_WCASE(8) PMM_WCASE(10) PMM_WCASE(12)
+    PMM_WCASE(14) PMM_WCASE(16) PMM_WCASE(18) PMM_WCASE(20) PMM_WCASE(22) PMM_WCASE(24)
+    PMM_WCASE(26) PMM_WCASE(28) PMM_WCASE(30)
+#undef PMM_WCASE
+    default: wait_vm<0>(); break;  // (never taken; safe)
+  }
+}
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// LDS fetch-and-increment in asm: hipcc waits vmcnt(0) before any LDS write
+// it sees while an LDS-DMA is in flight (it cannot tell the ring from the
+// counters), which would stall the epilogue wave on the ring's next K-steps
+__device__ __forceinline__ unsigned lds_inc(unsigned *p) {
+  unsigned r;
+  const uint32_t ad = (uint32_t)(size_t)(LDS_AS unsigned *)p;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(ad), "v"(1u) : "memory");
+  return r;
+}
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// MFMA with A (query fragment) from AGPRs and the accumulator in VGPRs (see
+// pmm_bf16_kernel.h for the hazard rules hipcc does not apply inside asm).
+__device__ __forceinline__ void mfma_acc(f32x16 &c, const bf16x8 &a, const bf16x8 &b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b) : "memory");
+}
+__device__ __forceinline__ void mfma_first(f32x16 &c, const bf16x8 &a, const bf16x8 &b) {
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b) : "memory");
+}
+__device__ __forceinline__ void mfma_drain(f32x16 (&acc)[NB]) {
+  asm volatile("s_nop 7\n\ts_nop 4" : "+v"(acc[0]), "+v"(acc[NB - 1]));
+#pragma unroll
+  for (int c = 1; c < NB - 1; c++) asm volatile("" : "+v"(acc[c]));
+}
+}  // namespace ws
+
+// Round barrier across the grid (speed only, bounded spin): the workgroups
+// of an XCD stream the same corpus tiles together.  Two __syncthreads, in
+// every wave of the workgroup; thread 0 (an MFMA wave) spins.
+__device__ __forceinline__ void round_sync(const GemmF32Args &a, unsigned target, int tid,
+                                           bool &sync_on, int *unit_l) {
+  if (!sync_on) return;
+  if (tid == 0) {
+    unsigned *round_bar = a.counter + 32;
+    atomicAdd(round_bar, 1u);
+    const uint64_t tstart = wall_clock64();
+    int ok = 1;
+    while (__hip_atomic_fetch_add(round_bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           target) {
+      __builtin_amdgcn_s_sleep(8);
+      if (wall_clock64() - tstart > (uint64_t)a.sync_timeout) {
+        ok = 0;
+        break;
+      }
+    }
+    if (!ok && a.stats) atomicAdd(a.stats + 2, 1ull);
+    *unit_l = ok;
+  }
+  __syncthreads();
+  sync_on = *unit_l != 0;
+  __syncthreads();
+}
+
+// Unit schedule.  Phase A: the first qb_full query blocks (a multiple of the
+// grid) are processed whole by one workgroup each, split by split in rounds
+// (round r: block (r / S) * grid + blockIdx.x, split r % S), so a row's
+// threshold and candidate buffer carry over from split to split (one
+// continuous top-k stream per row: about k ln(N / k) survivors instead of ~k
+// per split on top of a cold first split), while every workgroup of a round
+// still streams the same split (shared through the XCD's L2).  Phase B: the
+// remaining query blocks as independent (block, split) units, split-major,
+// each with its own candidate segment, seeded from the shared thresholds.
+struct UnitPos {
+  int qb, s, seg;     // query block, corpus split, candidate segment
+  bool first, last;   // first / last unit of the row state's run
+  unsigned target;    // round-barrier arrivals through this round
+};
+__device__ __forceinline__ bool unit_at(const GemmF32Args &a, int round, UnitPos &u) {
+  const int G = (int)gridDim.x;
+  const int rA = a.qb_full / G * a.S;
+  if (round < rA) {
+    u.qb = (round / a.S) * G + (int)blockIdx.x;
+    u.s = round % a.S;
+    u.seg = 0;
+    u.first = u.s == 0;
+    u.last = u.s == a.S - 1;
+    u.target = (unsigned)((round + 1) * G);
+    return true;
+  }
+  const int qbb = a.QB - a.qb_full;
+  const int nb = qbb * a.S;
+  const int idx = (round - rA) * G + (int)blockIdx.x;
+  if (idx >= nb) return false;
+  u.s = idx / qbb;
+  u.qb = a.qb_full + (idx - u.s * qbb);
+  u.seg = u.s;
+  u.first = u.last = true;
+  u.target = (unsigned)(rA * G + min((round - rA + 1) * G, nb));
+  return true;
+}
+
+// ===========================================================================
+// KS = padded D / 128 (K-steps per tile).
+// ===========================================================================
+template <int KS, int METRIC>
+__global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a) {
+  using namespace ws;
+  using C = Carve<KS>;
+  constexpr int NST = C::NST, NHB = C::NHB;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int *unit_l = (int *)(smem + OFF_UNIT);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const bool is_mfma = wid < NWM;
+  const int rw = is_mfma ? wid : wid - NWM;  // row group (32 rows) of this wave
+  const int r32 = lane & 31, h = lane >> 5;
+  constexpr bool XFORM = (METRIC != kMetricDot);
+  char *ring = smem + C::OFF_RING;
+
+  // The two roles run separate unit loops (identical trip counts and barrier
+  // sequences), so each role's loop-invariant values stay out of the other's
+  // registers.
+  bool sync_on = a.round_sync != 0;
+  // PMM_STATS: shader cycles per phase, per wave (a diagnostic build path;
+  // off, the memtime reads are skipped on a wave-uniform branch)
+#ifdef PMM_WS_STATS
+  const bool timing = a.stats != nullptr;
+#else
+  constexpr bool timing = false;  // (build with -DPMM_WS_STATS for the cycle stats)
+#endif
+  const uint64_t t_start = timing ? __builtin_amdgcn_s_memtime() : 0;
+  uint64_t cy0 = 0, cy1 = 0, cy2 = 0, cy3 = 0, nq = 0;
+  auto stamp = [&]() __attribute__((always_inline)) { return timing ? __builtin_amdgcn_s_memtime() : 0; };
+  if (is_mfma) {
+  bf16x8 af[KSUB * KS];  // this wave's query rows, kept across a run's units
+  for (int round = 0;; round++) {
+    UnitPos u;
+    if (!unit_at(a, round, u)) break;
+    round_sync(a, u.target, tid, sync_on, unit_l);
+    const int t0 = u.s * a.tps;
+    const int t1 = min(t0 + a.tps, a.ntiles);
+    const int wrow0 = u.qb * BM + rw * 32;
+      // ================= MFMA role =================
+      if (u.first) {
+        const __amdgpu_buffer_rsrc_t rq = make_rsrc(
+            a.qb + (int64_t)wrow0 * a.ldq, (int64_t)max(0, min(32, a.M - wrow0)) * a.ldq * 2);
+        const uint32_t qoff = (uint32_t)(r32 * a.ldq * 2 + 128 * h);
+        // the descriptor may be fresh from a VALU write (readfirstlane):
+        // 5 wait states before a VMEM instruction reads it (hipcc pads
+        // nothing in front of an asm statement)
+        asm volatile("s_nop 4" ::"s"(rq));
+#pragma unroll
+        for (int i = 0; i < KSUB * KS; i++)
+          asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen offset:%3"
+                       : "=v"(af[i])
+                       : "v"(qoff), "s"(rq), "i"(((i / KSUB) * 128 + (i % KSUB) * 8) * 2)
+                       : "memory");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      // LDS byte address of this lane's fragment chunk: column r32 of a group
+      // at r32 * KB, chunk (8h + sub) stored at chunk (8h + sub) ^ (r32 & 15);
+      // since 8h + sub = 8h ^ sub (sub < 8), substep sub's address is the
+      // sub-0 address XOR (sub << 4): one v_xor per substep, no per-substep
+      // address registers (the A rows leave ~60 VGPRs for everything else)
+      const uint32_t lane_off = (uint32_t)(r32 * KB + 16 * ((8 * h) ^ (r32 & 15)));
+      const uint32_t ring_lds = (uint32_t)(size_t)(LDS_AS char *)ring;
+      int sl = 0;
+      for (int tile = t0; tile < t1; tile++) {
+        f32x16 acc[NB];
+        bf16x8 bq[PF + 1][NB];  // fragment sets: PF in flight + the one in use
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+          wait_lgkm0();  // reads of the previous slot (and the hand-off writes) retired
+          barrier();     // B_g: step g landed
+          uint32_t sbase = ring_lds + (uint32_t)(sl * STAGE) + lane_off;
+          asm volatile("" : "+v"(sbase));  // keep the per-substep XORs in the loop
+          auto rd = [&](int sub, int set) __attribute__((always_inline)) {
+            const uint32_t ad = sbase ^ (uint32_t)(sub << 4);
+#pragma unroll
+            for (int c = 0; c < NB; c++) bq[set][c] = *(const LDS_AS bf16x8 *)(size_t)(ad + c * 32 * KB);
+          };
+          const int g0 = KSUB * ks;
+#pragma unroll
+          for (int p = 0; p < PF; p++) rd(p, (g0 + p) % (PF + 1));
+          // the previous step's last MFMA group, held back past the barrier:
+          // it covers the latency of the reads just issued
+          if (ks > 0) {
+#pragma unroll
+            for (int c = 0; c < NB; c++) mfma_acc(acc[c], af[g0 - 1], bq[(g0 - 1) % (PF + 1)][c]);
+          }
+#pragma unroll
+          for (int sub = 0; sub < KSUB; sub++) {
+            const int gs = g0 + sub;
+            if (sub + PF < KSUB) rd(sub + PF, (gs + PF) % (PF + 1));
+            if (!(sub == KSUB - 1 && ks < KS - 1)) {
+#pragma unroll
+              for (int c = 0; c < NB; c++) {
+                if (gs == 0) mfma_first(acc[c], af[0], bq[0][c]);
+                else mfma_acc(acc[c], af[gs], bq[gs % (PF + 1)][c]);
+              }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          sl = (sl == NST - 1) ? 0 : sl + 1;
+        }
+        mfma_drain(acc);
+        // hand the tile to the epilogue wave of these rows
+        char *hb = smem + OFF_HAND + ((tile % NHB) * NWM + rw) * HAND;
+#pragma unroll
+        for (int c = 0; c < NB; c++)
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            *(f32x4 *)(hb + ((c * 4 + q) * 64 + lane) * 16) =
+                (f32x4){acc[c][4 * q], acc[c][4 * q + 1], acc[c][4 * q + 2], acc[c][4 * q + 3]};
+      }
+      // the epilogue waves' last tile: two more barriers
+      wait_lgkm0();
+      barrier();
+      barrier();
+    }
+  } else {
+  for (int round = 0;; round++) {
+    UnitPos u;
+    if (!unit_at(a, round, u)) break;
+    round_sync(a, u.target, tid, sync_on, unit_l);
+    const int s = u.seg;  // candidate segment of this unit's rows
+    const int t0 = u.s * a.tps;
+    const int t1 = min(t0 + a.tps, a.ntiles);
+    const int wrow0 = u.qb * BM + rw * 32;
+      // ================= epilogue role =================
+      u64 *thr_w = (u64 *)(smem + OFF_THR) + rw * 32;
+      unsigned *cnt_w = (unsigned *)(smem + OFF_CNT) + rw * 32;
+      float *qex_w = (float *)(smem + OFF_QEX) + rw * 32;
+      float *lo_w = (float *)(smem + OFF_LO) + rw * 32;
+      float *cvr = (float *)(smem + OFF_CVR);
+      float *cnr = (float *)(smem + OFF_CNR);
+      u64 *scr = (u64 *)(smem + C::OFF_SCR) + (size_t)rw * a.capg;
+      if (u.first && lane < 32) {
+        const int grow = wrow0 + lane;
+        const float qv = (XFORM && grow < a.M) ? a.qn[grow] : 0.0f;
+        qex_w[lane] = qv;
+        const u64 t = (grow < a.M)
+                          ? __hip_atomic_load(a.gthr + grow, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                          : ~0ull;
+        thr_w[lane] = t;
+        lo_w[lane] = prefilter_bound<METRIC>(t, qv);
+        cnt_w[lane] = 0u;
+      }
+      wave_sync();
+      float lo[16];
+      auto load_lo = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int e = 0; e < 16; e++) lo[e] = lo_w[acc_row(e, h)];
+      };
+      load_lo();
+
+      // loop-invariant per-lane source offsets of this wave's corpus pieces:
+      // piece i = 4 tile columns x 256 B; chunk ch of column col lands in LDS
+      // chunk ch ^ (col & 15) (conflict-free ds_read_b128 fragment reads)
+      uint32_t b_voff[P];
+#pragma unroll
+      for (int i = 0; i < P; i++) {
+        const int col = (i * NWE + rw) * 4 + (lane >> 4);
+        const int ch = (lane & 15) ^ (col & 15);
+        b_voff[i] = (uint32_t)(col * a.ldc * 2 + ch * 16);
+      }
+      // one K-step's DMA: corpus pieces into ring slot `slot`, plus on a
+      // tile's first step this wave's share of its column factors / norms
+      auto stage = [&](int slot, int tile, int ks) __attribute__((always_inline)) {
+        if (a.ablate == 3) return;  // benchmarking only: no corpus traffic at all
+        const int col0 = tile * BN;
+        const __amdgpu_buffer_rsrc_t rb =
+            make_rsrc(a.cb + (int64_t)col0 * a.ldc, (int64_t)max(0, min(BN, a.N - col0)) * a.ldc * 2);
+        char *st = ring + slot * STAGE;
+        const uint32_t soff = (uint32_t)ks * (uint32_t)KB;
+#pragma unroll
+        for (int i = 0; i < P; i++) dma16(rb, st + (i * NWE + rw) * 1024, b_voff[i], soff);
+        if (XFORM && ks == 0) {
+          constexpr int PER = BN / NWE;
+          const int c0 = col0 + rw * PER;
+          const int64_t nb = (int64_t)max(0, min(PER, a.N - c0)) * 4;
+          const __amdgpu_buffer_rsrc_t rc = make_rsrc(a.cpre + c0, nb);
+          const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.cn + c0, nb);
+          const int o = (tile & (CVT - 1)) * BN + rw * PER;
+          if (lane < PER) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (LDS_AS void *)(cvr + o), 4,
+                                                     (uint32_t)(lane * 4), 0, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (LDS_AS void *)(cnr + o), 4,
+                                                     (uint32_t)(lane * 4), 0, 0, 0);
+          }
+        }
+      };
+
+      // Survivor queue (LDS, per wave): item = accumulator bits | (row in
+      // wave | global column << 5) << 32.  Survivors are re-scored exactly
+      // in 64-wide rounds (one item per lane) when the queue could overflow,
+      // every 4 tiles (the column-norm ring holds the last 8) and at the
+      // unit's end.  Queue writes are asm: hipcc would wait for the in-flight
+      // ring DMAs before every LDS store it sees.
+      const uint32_t lq_lds = (uint32_t)(size_t)(LDS_AS char *)(smem + C::OFF_QUEUE) + rw * QCAP * 8;
+      const u64 *lq = (const u64 *)(smem + C::OFF_QUEUE) + rw * QCAP;
+      int qlen = 0;  // wave-uniform
+      auto drain = [&]() __attribute__((always_inline)) {
+        if (timing) nq += (uint64_t)qlen;
+        for (int base = 0; base < qlen; base += 64) {
+          const int i = base + lane;
+          if (i < qlen) {
+            const u64 it = lq[i];
+            const float v = __uint_as_float((uint32_t)it);
+            const int rl = (int)((it >> 32) & 31u);
+            const int gcol = (int)(it >> 37);
+            const float cnv = XFORM ? cnr[((gcol / BN) & (CVT - 1)) * BN + (gcol % BN)] : 0.0f;
+            const float sc = exact_score<METRIC>(v, XFORM ? qex_w[rl] : 0.0f, cnv);
+            const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
+            const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
+            if (comp > thr_w[rl]) {
+              const unsigned pos = lds_inc(&cnt_w[rl]);
+              a.cand[((int64_t)(wrow0 + rl) * a.S + s) * a.capg + pos] = comp;
+            }
+          }
+          // a round adds at most 64 per row: compact every row that could
+          // overflow on the next round
+          wave_sync();
+          const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
+          u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 64));
+          if (need) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            while (need) {
+              const int r = __builtin_ctzll(need);
+              need &= need - 1;
+              compact_row(a, s, wrow0 + r, thr_w + r, cnt_w + r, scr, lane);
+            }
+            if (lane < 32) lo_w[lane] = prefilter_bound<METRIC>(thr_w[lane], qex_w[lane]);
+            wave_sync();
+            load_lo();
+          }
+        }
+        qlen = 0;
+      };
+
+      // epilogue of column group c of tile pt (accumulators in hand-off
+      // buffer pt & 1): the pre-filter difference of every score, their
+      // NaN-propagating max per lane, and only if some lane's max passes,
+      // the per-score survivor bits and their queueing
+      auto epilogue = [&](int pt, int c) __attribute__((always_inline)) {
+        const char *hb = smem + OFF_HAND + ((pt % NHB) * NWM + rw) * HAND;
+        f32x4 v4[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) v4[q] = *(const f32x4 *)(hb + ((c * 4 + q) * 64 + lane) * 16);
+        const int tc = 32 * c + r32;
+        const int gcol = pt * BN + tc;
+        const float cv = XFORM ? cvr[(pt & (CVT - 1)) * BN + tc] : 0.0f;
+        float d[16];
+#pragma unroll
+        for (int e = 0; e < 16; e++) d[e] = prefilter_diff<METRIC>(v4[e >> 2][e & 3], cv, lo[e]);
+        float dm = d[0];
+#pragma unroll
+        for (int e = 1; e < 16; e++) dm = __builtin_elementwise_maximum(dm, d[e]);
+        const bool any = !(dm < 0.0f) && gcol < a.N;
+        if (__ballot(any) == 0ull) return;
+        uint32_t bits = 0u;
+#pragma unroll
+        for (int e = 0; e < 16; e++) bits = (bits << 1) | (uint32_t)!(d[e] < 0.0f);
+        if (!any) bits = 0u;
+        const float *hf = (const float *)(hb + ((c * 4) * 64 + lane) * 16);
+        for (;;) {
+          const bool act = bits != 0u;
+          const u64 mk = __ballot(act);
+          if (mk == 0ull) break;
+          if (act) {
+            const int j = 31 - __builtin_clz(bits);  // bit j <-> e = 15 - j
+            bits &= ~(1u << j);
+            const int e = 15 - j;
+            const float v = hf[(e >> 2) * 256 + (e & 3)];
+            const uint32_t hi = (uint32_t)acc_row(e, h) | ((uint32_t)gcol << 5);
+            const u64 item = (u64)__float_as_uint(v) | ((u64)hi << 32);
+            asm volatile("ds_write_b64 %0, %1" ::"v"(lq_lds + (uint32_t)(qlen + lanes_below(mk)) * 8u),
+                         "v"(item)
+                         : "memory");
+          }
+          qlen += __popcll(mk);
+          if (qlen > QCAP - 64) {
+            wait_lgkm0();
+            drain();
+          }
+        }
+      };
+
+      // prologue: K-steps 0 .. NST-2 of the unit; step 0 landed before B_0
+#pragma unroll
+      for (int j = 0; j < NST - 1; j++) stage(j, t0 + j / KS, j % KS);
+      {
+        int n = 0;
+#pragma unroll
+        for (int j = 1; j < NST - 1; j++) n += step_dmas<XFORM>(j % KS);
+        wait_vm_n(n);
+      }
+      int sl = 0;
+      for (int tile = t0; tile < t1; tile++) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++) {
+          uint64_t tt = stamp();
+          barrier();  // B_g
+          if (timing) {
+            const uint64_t t2 = stamp();
+            cy3 += t2 - tt;
+            tt = t2;
+          }
+          {
+            // step g + NST - 1 into the slot of step g - 1 (read by every
+            // MFMA wave before B_g); past the unit's end a harmless read
+            constexpr int ahead = NST - 1;
+            const int slj = (sl == 0) ? NST - 1 : sl - 1;
+            stage(slj, tile + (ks + ahead) / KS, (ks + ahead) % KS);
+          }
+          if (timing) {
+            const uint64_t t2 = stamp();
+            cy0 += t2 - tt;
+            tt = t2;
+          }
+          if (tile > t0 && a.ablate != 1 && a.ablate != 3) {
+            if (KS == 1) {
+#pragma unroll
+              for (int c = 0; c < NB; c++) epilogue(tile - 1, c);
+            } else if (ks < NB) {
+              epilogue(tile - 1, ks);
+            }
+            if (ks == (KS == 1 ? 0 : NB - 1) && ((tile - t0) & 3) == 0 && qlen > 0) {
+              wait_lgkm0();
+              drain();
+            }
+          }
+          if (timing) {
+            const uint64_t t2 = stamp();
+            cy1 += t2 - tt;
+            tt = t2;
+          }
+          // step g + 1 landed; steps g + 2 .. g + NST - 1 may stay in flight
+          {
+            int n = 0;
+#pragma unroll
+            for (int j = 2; j < NST; j++) n += step_dmas<XFORM>((ks + j) % KS);
+            wait_vm_n(n);
+          }
+          if (timing) cy2 += stamp() - tt;
+          sl = (sl == NST - 1) ? 0 : sl + 1;
+        }
+      }
+      barrier();  // the last tile's accumulators are in LDS
+      if (a.ablate != 1 && a.ablate != 3) {
+#pragma unroll
+        for (int c = 0; c < NB; c++) epilogue(t1 - 1, c);
+        wait_lgkm0();
+        drain();
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ring DMAs past the unit's end
+      if (lane < 32) {
+        const int grow = wrow0 + lane;
+        if (u.last && grow < a.M) a.cnt[(int64_t)grow * a.S + s] = cnt_w[lane];
+      }
+      barrier();
+    }
+  }
+  if (timing && lane == 0) {
+    // MFMA waves: [0] cycles at barriers, [1] all; epilogue waves: [3] DMA
+    // issue, [4] epilogue, [5] vmcnt waits, [6] barriers, [7] all
+    const uint64_t all = __builtin_amdgcn_s_memtime() - t_start;
+    if (is_mfma) {
+      atomicAdd(a.stats + 1, (u64)all);  // (no per-phase stamps: the role has no spare registers)
+    } else {
+      atomicAdd(a.stats + 0, (u64)nq);
+      atomicAdd(a.stats + 3, (u64)cy0);
+      atomicAdd(a.stats + 4, (u64)cy1);
+      atomicAdd(a.stats + 5, (u64)cy2);
+      atomicAdd(a.stats + 6, (u64)cy3);
+      atomicAdd(a.stats + 7, (u64)all);
+    }
+  }
+}
+
+template <int KS, int METRIC>
+static hipError_t launch_bf16_ws_t(const GemmF32Args &a, int grid, size_t lds, hipStream_t s) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void *)gemm_bf16_ws_kernel<KS, METRIC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  gemm_bf16_ws_kernel<KS, METRIC><<<dim3(grid), dim3(ws::NTH), lds, s>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace pmm

@@ -167,14 +167,14 @@ struct Timed {
 // ---------------------------------------------------------------------------
 struct Plan {
   int variant = 0;
-  int QB = 0, T = 0, tps = 0, S = 0, units = 0, grid = 0, capg = 0, P = 0;
+  int QB = 0, T = 0, tps = 0, S = 0, units = 0, grid = 0, capg = 0, P = 0, qb_full = 0;
   size_t off_counter = 0, off_gthr = 0, off_cnt = 0, off_cand = 0, off_qn = 0, off_cn = 0;
   size_t off_wq = 0;
   size_t total = 0;
 };
 
 void plan_units(int64_t m, int64_t n, int bm, int bn, int cus, double unit_overhead, int64_t max_S,
-                Plan &p) {
+                Plan &p, bool whole_blocks = false) {
   p.QB = (int)cdiv(m, bm);
   p.T = (int)cdiv(n, bn);
   double best = 1e300;
@@ -184,7 +184,12 @@ void plan_units(int64_t m, int64_t n, int bm, int bn, int cus, double unit_overh
     if (S > max_S) continue;
     if (tps > 1 && cdiv(p.T, tps - 1) == S) continue;  // same S, fewer tiles: dominated
     const int64_t units = (int64_t)p.QB * S;
-    const int64_t rounds = cdiv(units, cus);
+    // whole_blocks (wave-specialised bf16 kernel): floor(QB / grid) * grid
+    // query blocks run whole, split by split, the rest as split units
+    const int64_t grid = std::min<int64_t>(units, cus);
+    const int64_t rounds = whole_blocks && p.QB >= grid
+                               ? (p.QB / grid) * S + cdiv((p.QB % grid) * S, grid)
+                               : cdiv(units, cus);
     const double cost = (double)rounds * (tps + unit_overhead) + 1e-4 * (double)S;
     if (cost < best) {
       best = cost;
@@ -195,6 +200,7 @@ void plan_units(int64_t m, int64_t n, int bm, int bn, int cus, double unit_overh
   p.S = (int)cdiv(p.T, p.tps);
   p.units = p.QB * p.S;
   p.grid = (int)std::min<int64_t>(p.units, cus);
+  p.qb_full = (whole_blocks && p.QB >= p.grid) ? (p.QB / p.grid) * p.grid : 0;
 }
 
 // Tile-shape variant: PMM_GEMM_VARIANT overrides; otherwise the preferred
@@ -218,21 +224,41 @@ int choose_variant(int mode, int capg, int64_t m = 1 << 30, int64_t n = 1 << 30,
   return 0;
 }
 
+// bf16 kernel choice: the wave-specialised kernel (pmm_bf16_ws_kernel.h)
+// whenever its LDS carve holds the compaction scratch (k <= 448);
+// PMM_BF16_WS=0 forces the one-wave-per-SIMD kernel (pmm_bf16_kernel.h).
+// Read per call, so tests can exercise both.
+bool bf16_ws_enabled(int capg, int64_t d) {
+  const char *e = getenv("PMM_BF16_WS");
+  if (e && atoi(e) == 0) return false;
+  const int dp = (int)(cdiv(d, kBf16DAlign) * kBf16DAlign);
+  return capg <= kBf16WsMaxCapg && gemm_bf16_ws_lds_bytes(capg, dp) <= 160 * 1024;
+}
+
 // compute = PMM_COMPUTE_F32: the f32 kernel (variant chosen by LDS fit);
-// PMM_COMPUTE_BF16: the bf16 kernel (variant -1, 128 x 128 tiles, 4 waves).
+// PMM_COMPUTE_BF16: the wave-specialised bf16 kernel (variant -2, 128 x 64
+// tiles, 8 waves) or the 4-wave one (variant -1, 128 x 128 tiles).
 int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p,
               int compute = PMM_COMPUTE_F32) {
   p.capg = next_pow2((int)k + 64, 128);
   const bool bf16 = compute == PMM_COMPUTE_BF16;
-  p.variant = bf16 ? -1 : choose_variant(0, p.capg, m, n, cus);
+  const bool ws = bf16 && bf16_ws_enabled(p.capg, d);
+  p.variant = bf16 ? (ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
   const int bm = bf16 ? kBf16BM : gemm_f32_bm(p.variant);
-  const int bn = bf16 ? kBf16BN : gemm_f32_bn(p.variant);
+  const int bn = bf16 ? (ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
   const size_t cand_budget = size_t(8) << 30;
   int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
   // a bf16 unit starts by loading its 128 query rows into registers (about
   // two tiles' worth of time): longer splits amortise it
-  plan_units(m, n, bm, bn, cus, bf16 ? 2.0 : 0.5, max_S, p);
+  // PMM_BF16_WHOLE=1: run floor(QB / grid) * grid query blocks whole (row
+  // state carried across splits: 46% fewer survivors at c4) -- measured 9%
+  // slower at c4 (the longer-lived candidate buffers compact twice as often,
+  // and a compaction is a global round trip + an LDS sort on the epilogue
+  // wave), so split units stay the default
+  const char *we = getenv("PMM_BF16_WHOLE");
+  const bool whole = ws && we && atoi(we) == 1;
+  plan_units(m, n, bm, bn, cus, bf16 ? (ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
   p.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
   size_t off = 0;
   p.off_counter = off;
@@ -500,6 +526,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
   char *w = (char *)ws;
   float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
   HIP_TRY(hipMemsetAsync(w, 0, p.off_gthr + (size_t)m * 8, s));
+  if (p.qb_full) HIP_TRY(hipMemsetAsync(w + p.off_cnt, 0, (size_t)m * p.S * 4, s));
   if (metric != kMetricDot) {
     const int sq = metric == kMetricEuclidean;
     Timed t("norms_bf16", s);
@@ -539,6 +566,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     a.pf = 1;
     static const int defer_env = getenv("PMM_BF16_DEFER") ? atoi(getenv("PMM_BF16_DEFER")) : 1;
     a.defer = defer_env;
+    a.qb_full = p.qb_full;
     static const int sync_env = getenv("PMM_BF16_SYNC") ? atoi(getenv("PMM_BF16_SYNC")) : 1;
     a.round_sync = sync_env;
     // round-barrier spin limit: workgroups of one round finish up to a few ms
@@ -555,12 +583,20 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     }
     {
       Timed t("gemm_bf16_topk", s);
-      HIP_TRY(launch_gemm_bf16(a, p.grid, s));
+      HIP_TRY(p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s) : launch_gemm_bf16(a, p.grid, s));
     }
     if (stats) {
       unsigned long long h[8];
       HIP_TRY(hipMemcpyAsync(h, stats_buf, 64, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
+      if (p.variant == -2)
+        fprintf(stderr,
+                "[pmm stats] gemm_bf16_ws: units %d, S %d, tps %d, sync timeouts %llu, survivors "
+                "%llu; MFMA-wave cycles %.3g; epilogue-wave cycles: DMA issue %.3g, epilogue "
+                "%.3g, vmcnt waits %.3g, barriers %.3g of %.3g\n",
+                p.units, p.S, p.tps, h[2], h[0], (double)h[1], (double)h[3], (double)h[4],
+                (double)h[5], (double)h[6], (double)h[7]);
+      else
       fprintf(stderr,
               "[pmm stats] gemm_bf16: queued %llu, LDS-queue tiles %llu, sync timeouts %llu, "
               "compactions %llu, units %d, S %d, tps %d; wave cycles: K-loop %.3g, extract %.3g, "

@@ -232,6 +232,16 @@ __device__ __forceinline__ float prefilter_bound(u64 thr, float qv) {
   return L - ((fabsf(qv) + hi) * 0x1p-18f + 0x1p-100f);
 }
 
+// Pre-filter difference of one score (bf16 kernels): >= 0 (or NaN) iff the
+// score may enter the row's top-k (see prefilter_bound); a rounded difference
+// keeps the sign of the exact one.
+template <int METRIC>
+__device__ __forceinline__ float prefilter_diff(float v, float cv, float lo) {
+  if (METRIC == kMetricDot) return v - lo;
+  if (METRIC == kMetricCosine) return fmaf(v, cv, -lo);
+  return fmaf(2.0f, v, -cv) - lo;
+}
+
 __device__ __forceinline__ int acc_row(int e, int h) { return (e & 3) + 8 * (e >> 2) + 4 * h; }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void *base, int64_t bytes) {

@@ -47,6 +47,8 @@ struct GemmF32Args {
   int sync_timeout;               // bf16 kernel: round-barrier spin limit (100 MHz ticks)
   int pf;                         // bf16 kernel: corpus-fragment prefetch depth (1 or 2 substeps)
   int defer;                      // bf16 kernel: hold each K-step's last MFMA group past the barrier
+  int qb_full;                    // wave-specialised bf16 kernel: query blocks processed whole
+                                  // (phase A; a multiple of the grid), the rest as split units
   unsigned long long *stats;      // PMM_STATS only: [queued, flagged groups, tiles, compactions]
 };
 
@@ -97,6 +99,13 @@ constexpr int kBf16DAlign = 128;
 constexpr int kBf16MaxCapg = 1024;  // LDS budget for the compaction scratch (k <= 960)
 hipError_t launch_gemm_bf16(const GemmF32Args &a, int grid, hipStream_t s);
 size_t gemm_bf16_lds_bytes(int capg, int nst);
+// Wave-specialised bf16 kernel (pmm_bf16_ws_kernel.h): 128 query rows x 64
+// corpus columns per tile, 4 MFMA waves + 4 epilogue waves.  Used when its
+// LDS (compaction scratch included) fits: capg <= kBf16WsMaxCapg.
+constexpr int kBf16WsBN = 64;
+constexpr int kBf16WsMaxCapg = 512;
+size_t gemm_bf16_ws_lds_bytes(int capg, int D);  // D = padded dimension
+hipError_t launch_gemm_bf16_ws(const GemmF32Args &a, int grid, hipStream_t s);
 // f32 rows -> bf16 (round to nearest even) with row stride ldd, columns
 // d..ldd-1 zero-filled.
 hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t lds, uint16_t *dst,

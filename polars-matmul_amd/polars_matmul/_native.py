@@ -15,7 +15,10 @@ import os
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libpmm.so")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                        # diagnostics only: PMM_LIB=libpmm_stats.so (make stats) adds the
+                        # bf16 kernels' per-phase cycle counters (PMM_STATS=1)
+                        os.environ.get("PMM_LIB", "libpmm.so"))
 
 PMM_OK = 0
 PMM_ERR_ARG = 1

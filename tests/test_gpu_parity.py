@@ -417,6 +417,19 @@ def test_bf16_ragged_shapes(pmm, m, n, d, k, metric):
     _bf16_truth_check(q, c, k, metric, idx, sc, f"bf16 {m}x{n}x{d} k={k} {metric}")
 
 
+@pytest.mark.parametrize("m,n,d,k", [(130, 257, 33, 7), (257, 4099, 200, 64), (300, 2000, 768, 100)])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_one_wave_per_simd_kernel(pmm, m, n, d, k, metric, monkeypatch):
+    # PMM_BF16_WS=0: the 4-wave kernel (pmm_bf16_kernel.h) on shapes the
+    # wave-specialised kernel serves by default (it still serves k > 448)
+    monkeypatch.setenv("PMM_BF16_WS", "0")
+    rs = np.random.RandomState(m + n + d + k)
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    idx, sc = gpu_topk_bf16(q, c, k, metric)
+    _bf16_truth_check(q, c, k, metric, idx, sc, f"bf16 classic {m}x{n}x{d} k={k} {metric}")
+
+
 def test_bf16_recall_vs_f32(pmm):
     # SURVEY 8c bf16 criterion: recall@k >= 0.95 against the f32 result
     rs = np.random.RandomState(31)
@@ -457,6 +470,55 @@ def test_bf16_device_api_many_splits(pmm):
     assert bool((got_true >= kth - 2e-5).all())
     assert float((osc.double() - got_true).abs().max()) < 1e-5
     assert float((got_i == ref_i).float().mean()) > 0.97
+
+
+@pytest.mark.parametrize("whole", ["0", "1"])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_bf16_whole_block_runs(pmm, metric, whole, monkeypatch):
+    # M >= 128 x grid query rows.  PMM_BF16_WHOLE=1: the wave-specialised
+    # kernel runs the first 256 query blocks whole (split by split, row state
+    # carried across splits) and the remaining 2 blocks as split units;
+    # default: every unit a split unit.  Every row vs float64 truth.
+    import torch
+
+    monkeypatch.setenv("PMM_BF16_WHOLE", whole)
+
+    n = _native()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(11)
+    m, N, d, k = 33000, 30000, 256, 50
+    q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
+    c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
+    oi = torch.empty((m, k), dtype=torch.int32, device=dev)
+    osc = torch.empty((m, k), dtype=torch.float32, device=dev)
+    n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS[metric],
+                       oi.data_ptr(), osc.data_ptr(),
+                       stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    cd = c.double()
+    got_i = oi.long()
+    assert int(got_i.min()) >= 0 and int(got_i.max()) < N
+    match = 0.0
+    for r0 in range(0, m, 8192):
+        qd = q[r0:r0 + 8192].double()
+        if metric == "cosine":
+            s = (qd @ cd.T) / (qd.norm(dim=1, keepdim=True) * cd.norm(dim=1)[None, :])
+            ref_s, ref_i = torch.topk(s, k, dim=1)
+        else:
+            s = torch.cdist(qd, cd)
+            ref_s, ref_i = torch.topk(s, k, dim=1, largest=False)
+        gi = got_i[r0:r0 + 8192]
+        got_true = torch.gather(s, 1, gi)
+        kth = ref_s[:, -1:]
+        if metric == "cosine":
+            assert bool((got_true >= kth - 2e-5).all())
+        else:
+            assert bool((got_true <= kth + 2e-4).all())
+        tol = 1e-5 if metric == "cosine" else 2e-4
+        assert float((osc[r0:r0 + 8192].double() - got_true).abs().max()) < tol
+        match += float((gi == ref_i).float().sum())
+    assert match / (m * k) > 0.97
 
 
 def test_bf16_limits_raise(pmm):
