@@ -46,6 +46,7 @@ CONFIGS = {
     "c1": (1_000, 10_000, 256, 10, "cosine", "f32"),
 }
 MFMA_PEAK_TFLOPS = {"f32": 157.3, "bf16": 2516.6}  # MI355X dense matrix peaks (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
 def log(*a):
@@ -254,6 +255,9 @@ def main():
     kern_ms, kern_n = _native.timing_read("gemm_bf16_topk" if bf16 else "gemm_f32_topk")
     merge_ms, merge_n = _native.timing_read("merge_topk")
     shard_ms, shard_n = _native.timing_read("merge_shards")
+    # algorithmic bytes of this rank's last merge pass (the reduction's HBM
+    # roofline), read from the workspace after the timed region
+    merge_bytes = _native.merge_bytes(ws.data_ptr(), M, n_loc, D, k, mid, compute) if merge_n else None
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -320,6 +324,22 @@ def main():
         "merge_ms_avg": round(merge_ms / merge_n, 3) if merge_n else None,
         "shard_merge_ms_avg": round(shard_ms / shard_n, 3) if shard_n else None,
     }
+    reduction = None
+    if merge_n and merge_bytes:
+        mavg = merge_ms / merge_n / 1000.0
+        gbs = merge_bytes / mavg / 1e9
+        reduction = {
+            "kernel": "merge_kernel (per-row merge of the split candidate buffers)",
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": merge_bytes,
+            "kernel_ms_avg": round(mavg * 1000.0, 3),
+        }
+        if shard_n:
+            # rank 0's k-way merge of the world x M x k (index, score) lists
+            sbytes = (world + 1) * M * k * 8
+            savg = shard_ms / shard_n / 1000.0
+            reduction["shard_merge"] = {"bytes_per_launch": sbytes, "kernel_ms_avg": round(savg * 1000.0, 3),
+                                        "achieved": round(sbytes / savg / 1e9, 1), "unit": "GB/s"}
     cpu = None
     if args.cpu_sample and world == 1:
         n_s = min(args.cpu_sample, M)
@@ -362,6 +382,7 @@ def main():
                    "corpus": N, "dim": D, "k": k, "metric": metric,
                    "parallelism": f"corpus-row-shard x{world}" if world > 1 else "single GPU"},
         "roofline": roofline,
+        "reduction_roofline": reduction,
         "cpu_baseline": cpu,
         "cpu_baseline_numpy": cpu_np,
         "boundary": boundary,

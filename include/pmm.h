@@ -114,6 +114,14 @@ int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64
 size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int metric,
                                 int compute);
 
+/* Algorithmic bytes of the last fused top-k's merge pass (merge_kernel) for
+ * this problem and workspace, read after the call completed: the split
+ * counts, the candidates the GEMM left, the shared thresholds and the m x k
+ * output.  Measurement only (the HBM-roofline line of the reduction,
+ * SURVEY 8d); synchronous. */
+int pmm_topk_merge_bytes(const void *workspace, int64_t m, int64_t n, int64_t d, int64_t k,
+                         int metric, int compute, uint64_t *bytes);
+
 /* Fused top-k over device buffers.  d is the logical dimension; ldq / ldc are
  * row strides in elements, multiples of 4 and >= roundup(d, 32), with columns
  * d..roundup(d, 32)-1 zero-filled and 16-byte-aligned bases (pmm_topk_f32 pads

@@ -727,6 +727,34 @@ size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int 
   return p.total;
 }
 
+int pmm_topk_merge_bytes(const void *workspace, int64_t m, int64_t n, int64_t d, int64_t k,
+                         int metric, int compute, uint64_t *bytes) {
+  if (!bytes) return fail(PMM_ERR_ARG, "null output");
+  *bytes = 0;
+  if (m <= 0 || k <= 0) return PMM_OK;
+  if (compute != PMM_COMPUTE_BF16 && k > kFusedMaxK)
+    return fail(PMM_ERR_UNSUPPORTED, "no merge pass on the materialised path (k > %d)", kFusedMaxK);
+  int dev;
+  int rc = ensure_device(&dev);
+  if (rc) return rc;
+  int cus = 256;
+  {
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if ((int)g_dev.size() > dev && g_dev[dev].probed) cus = g_dev[dev].cus;
+  }
+  Plan p;
+  plan_topk(m, n, d, k, metric, cus, p, compute);
+  // the merge reads every row's split counts and shared threshold, the
+  // candidates the GEMM left, and writes the m x k (index, score) lists
+  std::vector<unsigned> cnt((size_t)m * p.S);
+  HIP_TRY(hipMemcpy(cnt.data(), (const char *)workspace + p.off_cnt, cnt.size() * 4,
+                    hipMemcpyDeviceToHost));
+  uint64_t cands = 0;
+  for (unsigned c : cnt) cands += std::min<unsigned>(c, (unsigned)p.capg);
+  *bytes = (uint64_t)m * p.S * 4 + cands * 8 + (uint64_t)m * 8 + (uint64_t)m * k * 8;
+  return PMM_OK;
+}
+
 int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, int64_t ldc,
                         int64_t n, int64_t d, int64_t k, int metric, int compute,
                         uint32_t index_base, uint32_t *out_idx, float *out_score, void *workspace,

@@ -427,30 +427,64 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   u64 *scr = (u64 *)smem + (size_t)wid * a.P;
   u64 T = (LOADER == 0) ? a.gthr[row] : 0ull;
   int cnt = 0;
-  for (int s = 0; s < a.S; s++) {
-    const int n_s = (LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + s] : a.k_in;
+  // candidate i of list s as a composite key (0 = empty)
+  auto load_x = [&](int s, int i) __attribute__((always_inline)) -> u64 {
     const int64_t seg = (int64_t)row * a.S + s;
-    for (int i0 = 0; i0 < n_s; i0 += 64) {
-      const int i = i0 + lane;
-      u64 x = 0ull;
-      if (i < n_s) {
-        if (LOADER == 0) {
-          x = a.cand[seg * a.capg + i];
-        } else {
-          const uint32_t id = a.in_idx[seg * a.k_in + i];
-          const float sc = a.in_score[seg * a.k_in + i];
-          if (id != 0xFFFFFFFFu)
-            x = ((u64)okey32(a.metric == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~id);
+    if (LOADER == 0) return a.cand[seg * a.capg + i];
+    const uint32_t id = a.in_idx[seg * a.k_in + i];
+    const float sc = a.in_score[seg * a.k_in + i];
+    return id != 0xFFFFFFFFu ? ((u64)okey32(a.metric == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~id)
+                             : 0ull;
+  };
+  auto take = [&](u64 x) __attribute__((always_inline)) {
+    const bool keep = (x != 0ull) && (x >= T);
+    const u64 m = __ballot(keep);
+    const int pos = cnt + lanes_below(m);
+    if (keep) scr[pos] = x;
+    cnt += __popcll(m);
+    if (cnt > a.P - 64) {
+      wave_sync();
+      cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
+    }
+  };
+  if (a.S <= 64) {
+    // All list lengths in one load (lane s holds list s's), then the lists'
+    // 64-entry chunks as one flat sequence, MU chunk loads in flight at a
+    // time: the row's reads no longer wait on one another (HBM latency, not
+    // bandwidth, bounded the per-list loop).
+    constexpr int MU = 4;
+    const int nl = (lane < a.S) ? ((LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + lane] : a.k_in) : 0;
+    int s = 0, c = 0;
+    int ns = __builtin_amdgcn_readlane(nl, 0);
+    while (s < a.S && c >= ns) {  // first non-empty list
+      s++;
+      ns = (s < a.S) ? __builtin_amdgcn_readlane(nl, s) : 0;
+    }
+    while (s < a.S) {
+      u64 x[MU];
+#pragma unroll
+      for (int u = 0; u < MU; u++) {
+        x[u] = 0ull;
+        if (s < a.S) {
+          const int i = c + lane;
+          if (i < ns) x[u] = load_x(s, i);
+          c += 64;
+          while (s < a.S && c >= ns) {
+            s++;
+            c = 0;
+            ns = (s < a.S) ? __builtin_amdgcn_readlane(nl, s) : 0;
+          }
         }
       }
-      const bool keep = (x != 0ull) && (x >= T);
-      const u64 m = __ballot(keep);
-      const int pos = cnt + lanes_below(m);
-      if (keep) scr[pos] = x;
-      cnt += __popcll(m);
-      if (cnt > a.P - 64) {
-        wave_sync();
-        cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
+#pragma unroll
+      for (int u = 0; u < MU; u++) take(x[u]);
+    }
+  } else {
+    for (int s = 0; s < a.S; s++) {
+      const int n_s = (LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + s] : a.k_in;
+      for (int i0 = 0; i0 < n_s; i0 += 64) {
+        const int i = i0 + lane;
+        take(i < n_s ? load_x(s, i) : 0ull);
       }
     }
   }

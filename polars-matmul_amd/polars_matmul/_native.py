@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "pmm_matmul_f32",
     "pmm_matmul_f64",
     "pmm_topk_workspace_bytes",
+    "pmm_topk_merge_bytes",
     "pmm_topk_f32_device",
     "pmm_topk_bf16_device",
     "pmm_merge_topk_device",
@@ -94,6 +95,7 @@ _SIGS = {
     "pmm_matmul_f32": ([_vp, _i64, _vp, _i64, _i64, _vp], _i32),
     "pmm_matmul_f64": ([_vp, _i64, _vp, _i64, _i64, _vp], _i32),
     "pmm_topk_workspace_bytes": ([_i64, _i64, _i64, _i64, _i32, _i32], _sz),
+    "pmm_topk_merge_bytes": ([_vp, _i64, _i64, _i64, _i64, _i32, _i32, ctypes.POINTER(ctypes.c_uint64)], _i32),
     "pmm_topk_f32_device": (
         [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _i32, _u32, _vp, _vp, _vp, _sz, _vp],
         _i32,
@@ -215,6 +217,14 @@ def merge_device(idx_ptr: int, score_ptr: int, m: int, lists: int, k_in: int, k_
 
 def workspace_bytes(m: int, n: int, d: int, k: int, metric: int, compute: int = COMPUTE_F32) -> int:
     return int(_lib.pmm_topk_workspace_bytes(m, n, d, k, metric, compute))
+
+
+def merge_bytes(workspace_ptr: int, m: int, n: int, d: int, k: int, metric: int,
+                compute: int = COMPUTE_F32) -> int:
+    """Algorithmic bytes of the last fused top-k's merge pass (measurement only)."""
+    out = ctypes.c_uint64(0)
+    check(_lib.pmm_topk_merge_bytes(workspace_ptr, m, n, d, k, metric, compute, ctypes.byref(out)))
+    return int(out.value)
 
 
 def timing_enable(on: bool = True) -> None:

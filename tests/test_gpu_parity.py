@@ -300,6 +300,33 @@ def test_device_api_sharded_merge_equals_full(pmm):
     np.testing.assert_allclose(got_s, full_s, rtol=1e-6, atol=1e-6)
 
 
+def test_merge_bytes_counts_the_candidates_left(pmm):
+    # the reduction's algorithmic bytes (bench.py "reduction_roofline"):
+    # counts + thresholds + output, plus 8 B per candidate the GEMM left --
+    # at least k per row, at most S * capg per row
+    import torch
+
+    n = _native()
+    rs = np.random.RandomState(5)
+    m, N, d, k = 200, 6000, 64, 20
+    dev = torch.device("cuda:0")
+    tq = torch.from_numpy(rs.randn(m, d).astype(np.float32)).to(dev)
+    tc = torch.from_numpy(rs.randn(N, d).astype(np.float32)).to(dev)
+    wb = n.workspace_bytes(m, N, d, k, 0)
+    ws = torch.zeros(wb, dtype=torch.uint8, device=dev)
+    oi = torch.empty((m, k), dtype=torch.int32, device=dev)
+    osc = torch.empty((m, k), dtype=torch.float32, device=dev)
+    n.topk_device(tq.data_ptr(), d, m, tc.data_ptr(), d, N, d, k, 0, oi.data_ptr(), osc.data_ptr(),
+                  workspace=ws.data_ptr(), workspace_bytes=wb,
+                  stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    b = n.merge_bytes(ws.data_ptr(), m, N, d, k, 0)
+    fixed = m * 8 + m * k * 8
+    assert b >= fixed + m * k * 8 + m * 4
+    assert b <= fixed + m * 4 * N + m * N * 8
+    assert n.merge_bytes(ws.data_ptr(), 0, N, d, k, 0) == 0
+
+
 def test_device_corpus_handle_matches_host_api(pmm):
     # corpus uploaded once, many calls
     n = _native()
