@@ -300,6 +300,49 @@ def test_device_api_sharded_merge_equals_full(pmm):
     np.testing.assert_allclose(got_s, full_s, rtol=1e-6, atol=1e-6)
 
 
+def test_c5_shape_corpus_sharded_8way(pmm):
+    # BASELINE configs[4] (1M x 10M x 1024 cosine k=100 on 8 GPUs, corpus
+    # row-sharded) at a size one GPU checks in seconds: D = 1024, k = 100,
+    # 8 contiguous corpus shards (sharded.shard_bounds), per-shard fused top-k
+    # with index_base + the k-way merge == the unsharded fused top-k, and
+    # both == float64 truth
+    import torch
+
+    from golden.make_golden import truth_scores
+    from polars_matmul.sharded import shard_bounds
+
+    n = _native()
+    rs = np.random.RandomState(1024)
+    m, N, d, k, world = 96, 24_000, 1024, 100, 8
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(N, d).astype(np.float32)
+    full_i, full_s = gpu_topk(q, c, k, "cosine")
+    dev = torch.device("cuda:0")
+    tq = torch.from_numpy(q).to(dev)
+    gi = torch.empty((m, world, k), dtype=torch.int32, device=dev)
+    gs = torch.empty((m, world, k), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    for r in range(world):
+        a, b = shard_bounds(N, world, r)
+        tc = torch.from_numpy(c[a:b]).to(dev)
+        oi = torch.empty((m, k), dtype=torch.int32, device=dev)
+        osc = torch.empty((m, k), dtype=torch.float32, device=dev)
+        n.topk_device(tq.data_ptr(), d, m, tc.data_ptr(), d, b - a, d, k, 0, oi.data_ptr(), osc.data_ptr(),
+                      index_base=a, stream=stream)
+        gi[:, r] = oi
+        gs[:, r] = osc
+    mi = torch.empty((m, k), dtype=torch.int32, device=dev)
+    ms = torch.empty((m, k), dtype=torch.float32, device=dev)
+    n.merge_device(gi.data_ptr(), gs.data_ptr(), m, world, k, k, 0, mi.data_ptr(), ms.data_ptr(), stream=stream)
+    torch.cuda.synchronize()
+    got_i = mi.cpu().numpy().view(np.uint32)
+    got_s = ms.cpu().numpy()
+    # the same f32 arithmetic per (query, corpus row) whatever the shard
+    assert np.array_equal(got_i, full_i)
+    assert np.array_equal(got_s, full_s)
+    check_topk(got_i, got_s, truth_scores(q, c, "cosine"), True, label="c5-shape 8-way sharded")
+
+
 def test_merge_bytes_counts_the_candidates_left(pmm):
     # the reduction's algorithmic bytes (bench.py "reduction_roofline"):
     # counts + thresholds + output, plus 8 B per candidate the GEMM left --
