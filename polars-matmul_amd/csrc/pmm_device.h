@@ -84,6 +84,39 @@ __device__ inline void wave_sort_desc_u64(u64 *s, int P, int lane) {
   }
 }
 
+// Exact k-th largest of the keys a wave holds E per lane (0 = empty slot), by
+// bitwise construction from the most significant bit: the largest v with
+// #{x >= v} >= k.  One compare per key and one popcount per 64 keys per bit,
+// no LDS: far cheaper than sorting the buffer to find one rank.  The keys of
+// one row are distinct (the corpus index rides in the low bits), so exactly
+// k keys are >= the result when at least k are non-empty.
+template <int E>
+__device__ inline u64 wave_kth_u64(const u64 (&x)[E], int k) {
+  u64 v = 0ull;
+  for (int b = 63; b >= 0; b--) {
+    const u64 c = v | (1ull << b);
+    int cnt = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) cnt += __popcll(__ballot(x[e] >= c));
+    if (cnt >= k) v = c;
+  }
+  return v;
+}
+// Store the non-empty keys >= t of x packed (lane order) through st(pos, key);
+// returns their count.
+template <int E, typename Store>
+__device__ inline int wave_keep_ge(const u64 (&x)[E], u64 t, Store st, int lane) {
+  int base = 0;
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    const bool keep = x[e] != 0ull && x[e] >= t;
+    const u64 m = __ballot(keep);
+    if (keep) st(base + lanes_below(m), x[e]);
+    base += __popcll(m);
+  }
+  return base;
+}
+
 // 16-byte entry for the materialised (row-select) path: f64 keys need all
 // 64 bits, so the index rides alongside.
 struct __attribute__((aligned(16))) Ent {
@@ -262,6 +295,26 @@ __device__ inline void compact_row(const GemmF32Args &a, int s, int grow, u64 *t
   u64 *base = a.cand + ((int64_t)grow * a.S + s) * a.capg;
   const int n = (int)*cnt_slot;
   const int P = a.capg;
+  if (P <= 512 && n > a.k) {
+    // select, don't sort: the buffer is unordered; keep its best k and
+    // raise the threshold to the k-th
+    u64 x[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int i = lane + 64 * e;
+      x[e] = (i < n) ? __hip_atomic_load(base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    }
+    const u64 nt = wave_kth_u64<8>(x, a.k);  // (the ballots consumed every load)
+    wave_keep_ge<8>(x, nt, [&](int pos, u64 v) __attribute__((always_inline)) { base[pos] = v; }, lane);
+    wave_sync();
+    if (lane == 0) {
+      *cnt_slot = (unsigned)a.k;
+      if (nt > *thr_slot) *thr_slot = nt;
+      atomicMax(a.gthr + grow, nt);
+    }
+    wave_sync();
+    return;
+  }
   for (int i = lane; i < P; i += 64)
     scr[i] = (i < n) ? __hip_atomic_load(base + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                      : 0ull;

@@ -405,6 +405,18 @@ hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid
 //   loader 1: gathered per-shard (idx, score) lists [M][S][k_in] (multi-GPU).
 // ===========================================================================
 __device__ int merge_compact(u64 *scr, int cnt, int k, int P, u64 *T, int lane) {
+  if (P <= 512 && cnt > k) {
+    // select the k best (wave_kth_u64), keep them unordered
+    u64 x[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) x[e] = (lane + 64 * e < cnt) ? scr[lane + 64 * e] : 0ull;
+    wave_sync();  // every lane has read before any rewrites
+    const u64 t = wave_kth_u64<8>(x, k);
+    if (t > *T) *T = t;
+    cnt = wave_keep_ge<8>(x, t, [&](int pos, u64 v) __attribute__((always_inline)) { scr[pos] = v; }, lane);
+    wave_sync();
+    return cnt;
+  }
   for (int i = cnt + lane; i < P; i += 64) scr[i] = 0ull;
   wave_sync();
   wave_sort_desc_u64(scr, P, lane);
@@ -489,6 +501,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     }
   }
   wave_sync();
+  if (cnt > a.k_out && a.P <= 512) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
   const int P2 = min(a.P, next_pow2_dev(cnt));
   for (int i = cnt + lane; i < P2; i += 64) scr[i] = 0ull;
   wave_sync();
