@@ -84,23 +84,58 @@ __device__ inline void wave_sort_desc_u64(u64 *s, int P, int lane) {
   }
 }
 
-// Exact k-th largest of the keys a wave holds E per lane (0 = empty slot), by
-// bitwise construction from the most significant bit: the largest v with
-// #{x >= v} >= k.  One compare per key and one popcount per 64 keys per bit,
-// no LDS: far cheaper than sorting the buffer to find one rank.  The keys of
-// one row are distinct (the corpus index rides in the low bits), so exactly
-// k keys are >= the result when at least k are non-empty.
+__device__ __forceinline__ u64 wave_max_u64(u64 v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const u64 w = __shfl_xor(v, o);
+    v = v > w ? v : w;
+  }
+  return v;
+}
+__device__ __forceinline__ u64 wave_min_u64(u64 v) {
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const u64 w = __shfl_xor(v, o);
+    v = v < w ? v : w;
+  }
+  return v;
+}
+// Exact k-th largest of the keys a wave holds E per lane (0 = empty slot;
+// at least k non-empty), by bitwise construction from the most significant
+// bit where the keys differ: the largest v with #{x >= v} >= k, stopping as
+// soon as exactly k keys are >= v (the k-th is then the least of them).  One
+// compare per key and one popcount per 64 keys per bit, no LDS: far cheaper
+// than sorting the buffer to find one rank.  The keys of one row are
+// distinct (the corpus index rides in the low bits).
 template <int E>
 __device__ inline u64 wave_kth_u64(const u64 (&x)[E], int k) {
-  u64 v = 0ull;
-  for (int b = 63; b >= 0; b--) {
+  u64 mx = 0ull, mn = ~0ull;
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    if (x[e] > mx) mx = x[e];
+    if (x[e] != 0ull && x[e] < mn) mn = x[e];
+  }
+  mx = wave_max_u64(mx);
+  mn = wave_min_u64(mn);
+  if (mx == 0ull) return 0ull;
+  const u64 diff = mx ^ mn;
+  int b = diff ? 63 - __builtin_clzll(diff) : -1;
+  u64 v = (b >= 0) ? (mx & ~((2ull << b) - 1ull)) : mx;  // the keys' common prefix
+  for (; b >= 0; b--) {
     const u64 c = v | (1ull << b);
     int cnt = 0;
 #pragma unroll
     for (int e = 0; e < E; e++) cnt += __popcll(__ballot(x[e] >= c));
-    if (cnt >= k) v = c;
+    if (cnt >= k) {
+      v = c;
+      if (cnt == k) break;
+    }
   }
-  return v;
+  u64 t = ~0ull;
+#pragma unroll
+  for (int e = 0; e < E; e++)
+    if (x[e] >= v && x[e] < t) t = x[e];
+  return wave_min_u64(t);
 }
 // Store the non-empty keys >= t of x packed (lane order) through st(pos, key);
 // returns their count.
