@@ -240,7 +240,18 @@ bool bf16_ws_enabled(int capg, int64_t d) {
 // tiles, 8 waves) or the 4-wave one (variant -1, 128 x 128 tiles).
 int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p,
               int compute = PMM_COMPUTE_F32) {
+  // Candidate buffer capacity per (row, split): a compaction keeps k, so a
+  // bigger buffer compacts less often but prunes with an older threshold.
+  // With selection-based compaction (wave_kth_u64, capg <= 512) 1.5x the
+  // power of two measured best (c4 155 -> 151 ms, c3 1082 -> 1077 ms);
+  // beyond 512 the compaction sorts, which needs a power of two.
   p.capg = next_pow2((int)k + 64, 128);
+  if (p.capg * 3 / 2 <= 512) p.capg = p.capg * 3 / 2;
+  {
+    // experiment knob: candidate buffer capacity (>= k + 64, multiple of 8)
+    static const int cap_env = getenv("PMM_CAPG") ? atoi(getenv("PMM_CAPG")) : 0;
+    if (cap_env > 0 && k + 64 <= 512) p.capg = std::max<int>(((int)k + 64 + 7) / 8 * 8, std::min(cap_env, 512) / 8 * 8);
+  }
   const bool bf16 = compute == PMM_COMPUTE_BF16;
   const bool ws = bf16 && bf16_ws_enabled(p.capg, d);
   p.variant = bf16 ? (ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
