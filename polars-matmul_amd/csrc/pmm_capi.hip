@@ -262,13 +262,14 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
   // a bf16 unit starts by loading its 128 query rows into registers (about
   // two tiles' worth of time): longer splits amortise it
-  // PMM_BF16_WHOLE=1: run floor(QB / grid) * grid query blocks whole (row
-  // state carried across splits: 46% fewer survivors at c4) -- measured 9%
-  // slower at c4 (the longer-lived candidate buffers compact twice as often,
-  // and a compaction is a global round trip + an LDS sort on the epilogue
-  // wave), so split units stay the default
+  // Wave-specialised kernel: floor(QB / grid) * grid query blocks run whole
+  // (one workgroup carries a block's row state across all splits: 46% fewer
+  // survivors at c4), the rest as split units.  Measured 9% slower with the
+  // LDS-sort compaction (the longer-lived buffers compact twice as often);
+  // with selection-based compaction 2% faster at c4 (149.5 -> 146.8 ms) and
+  // the merge reads one segment per row.  PMM_BF16_WHOLE=0: split units only.
   const char *we = getenv("PMM_BF16_WHOLE");
-  const bool whole = ws && we && atoi(we) == 1;
+  const bool whole = ws && !(we && atoi(we) == 0);
   plan_units(m, n, bm, bn, cus, bf16 ? (ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
   p.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
   size_t off = 0;

@@ -62,6 +62,8 @@ if "FETCH_SIZE" in per and "WRITE_SIZE" in per:
     out["hbm_bytes_per_launch"] = out["hbm_read_bytes_per_launch"] + out["hbm_write_bytes_per_launch"]
 if "TCC_HIT_sum" in per:
     out["l2_hit_rate"] = per["TCC_HIT_sum"] / (per["TCC_HIT_sum"] + per["TCC_MISS_sum"])
-if "SQ_INSTS_VALU" in per and "SQ_INSTS_MFMA" in per:
+if "SQ_INSTS_VALU" in per and per.get("SQ_INSTS_MFMA"):
     out["valu_per_mfma"] = (per["SQ_INSTS_VALU"] - per["SQ_INSTS_MFMA"]) / per["SQ_INSTS_MFMA"]
+if "hbm_bytes_per_launch" in out and out.get("avg_ms"):
+    out["hbm_gbs"] = out["hbm_bytes_per_launch"] / (out["avg_ms"] / 1000.0) / 1e9
 print(json.dumps(out, indent=1))
