@@ -269,7 +269,11 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   // with selection-based compaction 2% faster at c4 (149.5 -> 146.8 ms) and
   // the merge reads one segment per row.  PMM_BF16_WHOLE=0: split units only.
   const char *we = getenv("PMM_BF16_WHOLE");
-  const bool whole = ws && !(we && atoi(we) == 0);
+  const char *fe = getenv("PMM_F32_WHOLE");
+  // f32 kernel: the same split of units (PMM_F32_WHOLE=0: split units only).
+  // At c3 the GEMM time is unchanged (1076 ms either way) and the merge reads
+  // 0.89 GB instead of 2.17 GB (0.40 vs 0.65 ms).
+  const bool whole = bf16 ? (ws && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
   plan_units(m, n, bm, bn, cus, bf16 ? (ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
   p.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
   size_t off = 0;
@@ -394,6 +398,8 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
   if (k <= kFusedMaxK) {
     Plan p;
     plan_topk(m, n, dp, k, metric, cus, p);
+    // whole query blocks first (see gemm_f32_kernel's unit decode)
+    const int64_t units = p.qb_full ? p.qb_full + (int64_t)(p.QB - p.qb_full) * p.S : p.units;
     if (!ws) {
       int rc = arena(dev, s, p.total, &ws);
       if (rc) return rc;
@@ -404,6 +410,7 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
     if (c_norms) cn = const_cast<float *>(c_norms);
     HIP_TRY(hipMemsetAsync(w, 0, p.off_gthr + (size_t)m * 8, s));
+    if (p.qb_full) HIP_TRY(hipMemsetAsync(w + p.off_cnt, 0, (size_t)m * p.S * 4, s));
     if (metric != kMetricDot) {
       const int sq = metric == kMetricEuclidean;
       Timed t("norms_f32", s);
@@ -428,7 +435,8 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     a.S = p.S;
     a.tps = p.tps;
     a.ntiles = p.T;
-    a.units = p.units;
+    a.units = (int)units;
+    a.qb_full = p.qb_full;
     a.counter = (unsigned *)(w + p.off_counter);
     {
       static const int ablate = getenv("PMM_ABLATE") ? atoi(getenv("PMM_ABLATE")) : 0;

@@ -147,10 +147,23 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     const int unit = *unit_l;
     __syncthreads();
     if (unit >= a.units) break;
-    const int s = unit / a.QB;
-    const int qb = unit - s * a.QB;
-    const int t0 = s * a.tps;
-    const int t1 = min(t0 + a.tps, a.ntiles);
+    // units [0, qb_full): whole query blocks (every tile, candidate segment
+    // 0: a row's threshold and buffer carry over the whole corpus); then the
+    // remaining blocks as (split, block) units, split-major
+    int s, qb, t0, t1;
+    if (MODE == 0 && unit < a.qb_full) {
+      qb = unit;
+      s = 0;
+      t0 = 0;
+      t1 = a.ntiles;
+    } else {
+      const int u2 = MODE == 0 ? unit - a.qb_full : unit;
+      const int qbb = MODE == 0 ? a.QB - a.qb_full : a.QB;
+      s = u2 / qbb;
+      qb = (MODE == 0 ? a.qb_full : 0) + (u2 - s * qbb);
+      t0 = s * a.tps;
+      t1 = min(t0 + a.tps, a.ntiles);
+    }
     const int wrow0 = qb * G::BM + wid * 32;
     const __amdgpu_buffer_rsrc_t ra =
         make_rsrc(a.q + (int64_t)wrow0 * a.ldq, (int64_t)min(32, a.M - wrow0) * a.ldq * 4);
