@@ -240,6 +240,13 @@ bool bf16_ws_enabled(int capg, int64_t d) {
 // tiles, 8 waves) or the 4-wave one (variant -1, 128 x 128 tiles).
 int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p,
               int compute = PMM_COMPUTE_F32) {
+  // testing knob: plan for fewer workgroups (small problems then take the
+  // whole-query-block schedule that only full-size runs reach otherwise);
+  // read per call so a test can set and clear it
+  if (const char *ce = getenv("PMM_CUS")) {
+    const int c = atoi(ce);
+    if (c > 0 && c < cus) cus = c;
+  }
   // Candidate buffer capacity per (row, split): a compaction keeps k, so a
   // bigger buffer compacts less often but prunes with an older threshold.
   // With selection-based compaction (wave_kth_u64, capg <= 512) 1.5x the

@@ -343,6 +343,35 @@ def test_c5_shape_corpus_sharded_8way(pmm):
     check_topk(got_i, got_s, truth_scores(q, c, "cosine"), True, label="c5-shape 8-way sharded")
 
 
+@pytest.mark.parametrize("compute", ["f32", "bf16"])
+def test_whole_query_block_schedule(pmm, compute, monkeypatch):
+    # the schedule full-size runs take (query blocks >= grid: whole blocks
+    # carry their rows' state over every corpus tile, then split units),
+    # forced at a checkable size by planning for 8 workgroups
+    from golden.make_golden import truth_scores
+    from parity import round_bf16
+
+    n = _native()
+    rs = np.random.RandomState(77)
+    m, N, d, k = 2500, 9000, 768, 50
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(N, d).astype(np.float32)
+    monkeypatch.setenv("PMM_CUS", "8")
+    for metric in ("cosine", "euclidean"):
+        if compute == "f32":
+            idx, sc = gpu_topk(q, c, k, metric)
+            truth = truth_scores(q, c, metric)
+        else:
+            idx, sc = gpu_topk_bf16(q, c, k, metric)
+            truth = truth_scores(round_bf16(q), round_bf16(c), metric)
+        check_topk(idx, sc, truth, metric != "euclidean", label=f"whole-block {compute} {metric}")
+    monkeypatch.delenv("PMM_CUS")
+    want = gpu_topk(q, c, k, "cosine") if compute == "f32" else gpu_topk_bf16(q, c, k, "cosine")
+    monkeypatch.setenv("PMM_CUS", "8")
+    got = gpu_topk(q, c, k, "cosine") if compute == "f32" else gpu_topk_bf16(q, c, k, "cosine")
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+
+
 def test_merge_bytes_counts_the_candidates_left(pmm):
     # the reduction's algorithmic bytes (bench.py "reduction_roofline"):
     # counts + thresholds + output, plus 8 B per candidate the GEMM left --
