@@ -390,6 +390,76 @@ int gemm_store_f32(const float *q, int64_t ldq, int64_t rows, const float *c, in
   return PMM_OK;
 }
 
+// One fused top-k pass (gemm_f32_kernel + merge_kernel) over a planned
+// workspace whose work counter and shared thresholds are already set.
+struct FusedF32 {
+  const float *q;
+  int64_t ldq, m;
+  const float *c;
+  int64_t ldc, n, dp, k;
+  int metric;
+  const float *qn, *cn, *cpre;
+};
+hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t index_base,
+                         uint32_t *out_idx, float *out_score, const char *gemm_label,
+                         const char *merge_label, hipStream_t s) {
+  // whole query blocks first (see gemm_f32_kernel's unit decode)
+  const int64_t units = p.qb_full ? p.qb_full + (int64_t)(p.QB - p.qb_full) * p.S : p.units;
+  if (p.qb_full) {
+    hipError_t e = hipMemsetAsync(w + p.off_cnt, 0, (size_t)f.m * p.S * 4, s);
+    if (e != hipSuccess) return e;
+  }
+  GemmF32Args a{};
+  a.q = f.q;
+  a.c = f.c;
+  a.qn = f.qn;
+  a.cn = f.cn;
+  a.cpre = f.cpre;
+  a.ldq = f.ldq;
+  a.ldc = f.ldc;
+  a.M = (int)f.m;
+  a.N = (int)f.n;
+  a.D = (int)f.dp;
+  a.k = (int)f.k;
+  a.capg = p.capg;
+  a.metric = f.metric;
+  a.QB = p.QB;
+  a.S = p.S;
+  a.tps = p.tps;
+  a.ntiles = p.T;
+  a.units = (int)units;
+  a.qb_full = p.qb_full;
+  a.counter = (unsigned *)(w + p.off_counter);
+  {
+    static const int ablate = getenv("PMM_ABLATE") ? atoi(getenv("PMM_ABLATE")) : 0;
+    a.ablate = ablate;
+  }
+  a.cand = (unsigned long long *)(w + p.off_cand);
+  a.wq = (unsigned long long *)(w + p.off_wq);
+  a.cnt = (unsigned *)(w + p.off_cnt);
+  a.gthr = (unsigned long long *)(w + p.off_gthr);
+  {
+    Timed t(gemm_label, s);
+    hipError_t e = launch_gemm_f32(a, p.variant, 0, p.grid, s);
+    if (e != hipSuccess) return e;
+  }
+  MergeArgs ma{};
+  ma.cand = a.cand;
+  ma.cnt = a.cnt;
+  ma.gthr = a.gthr;
+  ma.capg = p.capg;
+  ma.M = (int)f.m;
+  ma.S = p.S;
+  ma.k_out = (int)f.k;
+  ma.P = p.P;
+  ma.metric = f.metric;
+  ma.index_base = index_base;
+  ma.out_idx = out_idx;
+  ma.out_score = out_score;
+  Timed t(merge_label, s);
+  return launch_merge(ma, 0, s);
+}
+
 // c_norms: optional precomputed corpus norms for `metric` laid out as
 // [n norms | n pre-filter factors] (a pmm_corpus handle's cache); NULL =
 // compute them in this call.
@@ -405,8 +475,6 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
   if (k <= kFusedMaxK) {
     Plan p;
     plan_topk(m, n, dp, k, metric, cus, p);
-    // whole query blocks first (see gemm_f32_kernel's unit decode)
-    const int64_t units = p.qb_full ? p.qb_full + (int64_t)(p.QB - p.qb_full) * p.S : p.units;
     if (!ws) {
       int rc = arena(dev, s, p.total, &ws);
       if (rc) return rc;
@@ -417,63 +485,45 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
     if (c_norms) cn = const_cast<float *>(c_norms);
     HIP_TRY(hipMemsetAsync(w, 0, p.off_gthr + (size_t)m * 8, s));
-    if (p.qb_full) HIP_TRY(hipMemsetAsync(w + p.off_cnt, 0, (size_t)m * p.S * 4, s));
     if (metric != kMetricDot) {
       const int sq = metric == kMetricEuclidean;
       Timed t("norms_f32", s);
       HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
       if (!c_norms) HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, cn + n, s));
     }
-    GemmF32Args a{};
-    a.q = q;
-    a.c = c;
-    a.qn = qn;
-    a.cn = cn;
-    a.cpre = cn + n;
-    a.ldq = ldq;
-    a.ldc = ldc;
-    a.M = (int)m;
-    a.N = (int)n;
-    a.D = (int)dp;
-    a.k = (int)k;
-    a.capg = p.capg;
-    a.metric = metric;
-    a.QB = p.QB;
-    a.S = p.S;
-    a.tps = p.tps;
-    a.ntiles = p.T;
-    a.units = (int)units;
-    a.qb_full = p.qb_full;
-    a.counter = (unsigned *)(w + p.off_counter);
-    {
-      static const int ablate = getenv("PMM_ABLATE") ? atoi(getenv("PMM_ABLATE")) : 0;
-      a.ablate = ablate;
+    FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
+    // Threshold seeding.  When every unit spans few corpus tiles (small
+    // problems: the reference's own benchmark size), a unit starts cold and
+    // most of its time goes to exact re-scores and compactions of the scores
+    // that fill its rows' buffers.  A first fused pass over the corpus's first
+    // ns rows gives each row the k-th best of that sample; since the same
+    // kernel computes the same f32 score for a (query, corpus row) pair in
+    // either pass, (its composite key - 1) is an exact lower bound of the
+    // row's final k-th best, and seeds the shared threshold.
+    const int64_t ns = std::min<int64_t>(n, next_pow2((int)std::max<int64_t>(256, 8 * k), 256));
+    const char *se = getenv("PMM_SEED");
+    const bool want_seed = se ? atoi(se) != 0
+                              : ((int64_t)p.tps * gemm_f32_bn(p.variant) < 8192 && n >= 4 * ns);
+    if (want_seed && ns >= k && ns < n) {
+      Plan ps;
+      plan_topk(m, ns, dp, k, metric, cus, ps);
+      const size_t off_oi = al256(ps.total), off_os = al256(off_oi + (size_t)m * k * 4);
+      const size_t need = off_os + (size_t)m * k * 4;
+      // carved from the main candidate buffers (unused until the main pass)
+      if (need <= p.off_qn - p.off_cand) {
+        char *ws_seed = w + p.off_cand;
+        uint32_t *si = (uint32_t *)(ws_seed + off_oi);
+        float *ss = (float *)(ws_seed + off_os);
+        FusedF32 fs = f;
+        fs.n = ns;
+        HIP_TRY(hipMemsetAsync(ws_seed, 0, ps.off_gthr + (size_t)m * 8, s));
+        HIP_TRY(run_fused_f32(fs, ps, ws_seed, 0u, si, ss, "gemm_f32_seed", "merge_seed", s));
+        HIP_TRY(launch_seed_threshold(si, ss, (int)m, (int)k, metric,
+                                      (unsigned long long *)(w + p.off_gthr), s));
+      }
     }
-    a.cand = (unsigned long long *)(w + p.off_cand);
-    a.wq = (unsigned long long *)(w + p.off_wq);
-    a.cnt = (unsigned *)(w + p.off_cnt);
-    a.gthr = (unsigned long long *)(w + p.off_gthr);
-    {
-      Timed t("gemm_f32_topk", s);
-      HIP_TRY(launch_gemm_f32(a, p.variant, 0, p.grid, s));
-    }
-    MergeArgs ma{};
-    ma.cand = a.cand;
-    ma.cnt = a.cnt;
-    ma.gthr = a.gthr;
-    ma.capg = p.capg;
-    ma.M = (int)m;
-    ma.S = p.S;
-    ma.k_out = (int)k;
-    ma.P = p.P;
-    ma.metric = metric;
-    ma.index_base = index_base;
-    ma.out_idx = out_idx;
-    ma.out_score = out_score;
-    {
-      Timed t("merge_topk", s);
-      HIP_TRY(launch_merge(ma, 0, s));
-    }
+    HIP_TRY(hipMemsetAsync(w, 0, 256, s));  // the work counter (thresholds stay)
+    HIP_TRY(run_fused_f32(f, p, w, index_base, out_idx, out_score, "gemm_f32_topk", "merge_topk", s));
     return PMM_OK;
   }
   // k beyond the fused path: materialise score chunks, row-select them.
