@@ -405,10 +405,7 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
                          const char *merge_label, hipStream_t s) {
   // whole query blocks first (see gemm_f32_kernel's unit decode)
   const int64_t units = p.qb_full ? p.qb_full + (int64_t)(p.QB - p.qb_full) * p.S : p.units;
-  if (p.qb_full) {
-    hipError_t e = hipMemsetAsync(w + p.off_cnt, 0, (size_t)f.m * p.S * 4, s);
-    if (e != hipSuccess) return e;
-  }
+  // the caller has zeroed [w, w + p.off_cand): counter, thresholds, counts
   GemmF32Args a{};
   a.q = f.q;
   a.c = f.c;
@@ -484,14 +481,6 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     char *w = (char *)ws;
     float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
     if (c_norms) cn = const_cast<float *>(c_norms);
-    HIP_TRY(hipMemsetAsync(w, 0, p.off_gthr + (size_t)m * 8, s));
-    if (metric != kMetricDot) {
-      const int sq = metric == kMetricEuclidean;
-      Timed t("norms_f32", s);
-      HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
-      if (!c_norms) HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, cn + n, s));
-    }
-    FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
     // Threshold seeding.  When every unit spans few corpus tiles (small
     // problems: the reference's own benchmark size), a unit starts cold and
     // most of its time goes to exact re-scores and compactions of the scores
@@ -499,30 +488,43 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     // ns rows gives each row the k-th best of that sample; since the same
     // kernel computes the same f32 score for a (query, corpus row) pair in
     // either pass, (its composite key - 1) is an exact lower bound of the
-    // row's final k-th best, and seeds the shared threshold.
-    const int64_t ns = std::min<int64_t>(n, next_pow2((int)std::max<int64_t>(256, 8 * k), 256));
+    // row's final k-th best, and seeds the shared threshold.  The seed pass
+    // costs about as much at ns = 64 as at 1024 (c1: few workgroups, latency
+    // bound); 512 measured best by 1-2%.
+    int64_t ns = std::min<int64_t>(n, next_pow2((int)std::max<int64_t>(512, 8 * k), 256));
+    if (const char *ne = getenv("PMM_SEED_NS")) ns = std::min<int64_t>(n, std::max<int64_t>(atoll(ne), k));
     const char *se = getenv("PMM_SEED");
-    const bool want_seed = se ? atoi(se) != 0
-                              : ((int64_t)p.tps * gemm_f32_bn(p.variant) < 8192 && n >= 4 * ns);
-    if (want_seed && ns >= k && ns < n) {
-      Plan ps;
+    bool seed = (se ? atoi(se) != 0 : ((int64_t)p.tps * gemm_f32_bn(p.variant) < 8192 && n >= 4 * ns)) &&
+                ns >= k && ns < n;
+    Plan ps;
+    size_t off_oi = 0, off_os = 0;
+    if (seed) {
       plan_topk(m, ns, dp, k, metric, cus, ps);
-      const size_t off_oi = al256(ps.total), off_os = al256(off_oi + (size_t)m * k * 4);
-      const size_t need = off_os + (size_t)m * k * 4;
+      off_oi = al256(ps.total);
+      off_os = al256(off_oi + (size_t)m * k * 4);
       // carved from the main candidate buffers (unused until the main pass)
-      if (need <= p.off_qn - p.off_cand) {
-        char *ws_seed = w + p.off_cand;
-        uint32_t *si = (uint32_t *)(ws_seed + off_oi);
-        float *ss = (float *)(ws_seed + off_os);
-        FusedF32 fs = f;
-        fs.n = ns;
-        HIP_TRY(hipMemsetAsync(ws_seed, 0, ps.off_gthr + (size_t)m * 8, s));
-        HIP_TRY(run_fused_f32(fs, ps, ws_seed, 0u, si, ss, "gemm_f32_seed", "merge_seed", s));
-        HIP_TRY(launch_seed_threshold(si, ss, (int)m, (int)k, metric,
-                                      (unsigned long long *)(w + p.off_gthr), s));
-      }
+      seed = off_os + (size_t)m * k * 4 <= p.off_qn - p.off_cand;
     }
-    HIP_TRY(hipMemsetAsync(w, 0, 256, s));  // the work counter (thresholds stay)
+    // one fill zeroes the work counters, thresholds and buffer counts of the
+    // main pass [0, off_cand) and of the seed pass right behind it
+    HIP_TRY(hipMemsetAsync(w, 0, p.off_cand + (seed ? ps.off_cand : 0), s));
+    if (metric != kMetricDot) {
+      const int sq = metric == kMetricEuclidean;
+      Timed t("norms_f32", s);
+      HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
+      if (!c_norms) HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, cn + n, s));
+    }
+    FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
+    if (seed) {
+      char *ws_seed = w + p.off_cand;
+      uint32_t *si = (uint32_t *)(ws_seed + off_oi);
+      float *ss = (float *)(ws_seed + off_os);
+      FusedF32 fs = f;
+      fs.n = ns;
+      HIP_TRY(run_fused_f32(fs, ps, ws_seed, 0u, si, ss, "gemm_f32_seed", "merge_seed", s));
+      HIP_TRY(launch_seed_threshold(si, ss, (int)m, (int)k, metric,
+                                    (unsigned long long *)(w + p.off_gthr), s));
+    }
     HIP_TRY(run_fused_f32(f, p, w, index_base, out_idx, out_score, "gemm_f32_topk", "merge_topk", s));
     return PMM_OK;
   }
