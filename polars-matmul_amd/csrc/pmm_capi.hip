@@ -400,9 +400,11 @@ struct FusedF32 {
   int metric;
   const float *qn, *cn, *cpre;
 };
+// seed_gthr != NULL: the merge raises those thresholds instead of writing lists.
 hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t index_base,
                          uint32_t *out_idx, float *out_score, const char *gemm_label,
-                         const char *merge_label, hipStream_t s) {
+                         const char *merge_label, hipStream_t s,
+                         unsigned long long *seed_gthr = nullptr) {
   // whole query blocks first (see gemm_f32_kernel's unit decode)
   const int64_t units = p.qb_full ? p.qb_full + (int64_t)(p.QB - p.qb_full) * p.S : p.units;
   // the caller has zeroed [w, w + p.off_cand): counter, thresholds, counts
@@ -453,6 +455,7 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
   ma.index_base = index_base;
   ma.out_idx = out_idx;
   ma.out_score = out_score;
+  ma.seed_gthr = seed_gthr;
   Timed t(merge_label, s);
   return launch_merge(ma, 0, s);
 }
@@ -497,13 +500,10 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     bool seed = (se ? atoi(se) != 0 : ((int64_t)p.tps * gemm_f32_bn(p.variant) < 8192 && n >= 4 * ns)) &&
                 ns >= k && ns < n;
     Plan ps;
-    size_t off_oi = 0, off_os = 0;
     if (seed) {
       plan_topk(m, ns, dp, k, metric, cus, ps);
-      off_oi = al256(ps.total);
-      off_os = al256(off_oi + (size_t)m * k * 4);
       // carved from the main candidate buffers (unused until the main pass)
-      seed = off_os + (size_t)m * k * 4 <= p.off_qn - p.off_cand;
+      seed = ps.total <= p.off_qn - p.off_cand;
     }
     // one fill zeroes the work counters, thresholds and buffer counts of the
     // main pass [0, off_cand) and of the seed pass right behind it
@@ -516,14 +516,10 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     }
     FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
     if (seed) {
-      char *ws_seed = w + p.off_cand;
-      uint32_t *si = (uint32_t *)(ws_seed + off_oi);
-      float *ss = (float *)(ws_seed + off_os);
       FusedF32 fs = f;
       fs.n = ns;
-      HIP_TRY(run_fused_f32(fs, ps, ws_seed, 0u, si, ss, "gemm_f32_seed", "merge_seed", s));
-      HIP_TRY(launch_seed_threshold(si, ss, (int)m, (int)k, metric,
-                                    (unsigned long long *)(w + p.off_gthr), s));
+      HIP_TRY(run_fused_f32(fs, ps, w + p.off_cand, 0u, nullptr, nullptr, "gemm_f32_seed", "merge_seed", s,
+                            (unsigned long long *)(w + p.off_gthr)));
     }
     HIP_TRY(run_fused_f32(f, p, w, index_base, out_idx, out_score, "gemm_f32_topk", "merge_topk", s));
     return PMM_OK;

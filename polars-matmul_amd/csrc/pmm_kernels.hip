@@ -519,6 +519,13 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   for (int i = cnt + lane; i < P2; i += 64) scr[i] = 0ull;
   wave_sync();
   wave_sort_desc_u64(scr, P2, lane);
+  if (a.seed_gthr) {
+    if (lane == 0 && cnt >= a.k_out) {
+      const u64 x = scr[a.k_out - 1];
+      if (x != 0ull && x - 1 > a.seed_gthr[row]) a.seed_gthr[row] = x - 1;
+    }
+    return;
+  }
   for (int j = lane; j < a.k_out; j += 64) {
     const u64 x = (j < cnt) ? scr[j] : 0ull;
     uint32_t id = 0xFFFFFFFFu;
@@ -534,28 +541,6 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
 }
 
 size_t merge_lds_bytes_per_wave(int P) { return (size_t)P * 8; }
-
-// Threshold seeding (topk_f32_device_impl): row r's shared threshold becomes
-// (composite key of the k-th entry of a sample top-k) - 1, a lower bound of
-// the k-th best over the whole corpus, unless it is already higher.
-__global__ __launch_bounds__(256) void seed_threshold_kernel(const uint32_t *__restrict__ idx,
-                                                              const float *__restrict__ score, int m,
-                                                              int k, int metric, u64 *gthr) {
-  const int row = blockIdx.x * blockDim.x + threadIdx.x;
-  if (row >= m) return;
-  const uint32_t id = idx[(int64_t)row * k + k - 1];
-  if (id == 0xFFFFFFFFu) return;  // fewer than k in the sample
-  const float v = score[(int64_t)row * k + k - 1];
-  const u64 comp = ((u64)okey32(metric == kMetricEuclidean ? -v : v) << 32) | (u64)(~id);
-  if (comp == 0ull) return;
-  if (comp - 1 > gthr[row]) gthr[row] = comp - 1;
-}
-hipError_t launch_seed_threshold(const uint32_t *idx, const float *score, int m, int k, int metric,
-                                 unsigned long long *gthr, hipStream_t s) {
-  if (m <= 0 || k <= 0) return hipSuccess;
-  seed_threshold_kernel<<<(m + 255) / 256, 256, 0, s>>>(idx, score, m, k, metric, gthr);
-  return hipGetLastError();
-}
 
 hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
