@@ -652,3 +652,27 @@ def test_bf16_numpy_api_and_sharded_runner(pmm):
     torch.cuda.synchronize()
     assert np.array_equal(oi.cpu().numpy().view(np.uint32), i1)
     assert np.array_equal(osc.cpu().numpy().astype(np.float64), s1)
+
+
+@pytest.mark.parametrize("k", [1, 10, 100])
+def test_threshold_seeding_changes_nothing(pmm, k, monkeypatch):
+    # small problems run a seed pass over the corpus's first rows and start
+    # the main pass from (its k-th composite key - 1); the result must equal
+    # the unseeded run bit for bit, ties (duplicated corpus rows) included
+    from golden.make_golden import truth_scores
+
+    rs = np.random.RandomState(31 + k)
+    m, N, d = 700, 9000, 256
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(N, d).astype(np.float32)
+    c[4000:4600] = c[:600]  # duplicates of sampled rows, later in the corpus
+    for metric in ("cosine", "dot", "euclidean"):
+        monkeypatch.setenv("PMM_SEED", "0")
+        want = gpu_topk(q, c, k, metric)
+        monkeypatch.setenv("PMM_SEED", "1")
+        got = gpu_topk(q, c, k, metric)
+        monkeypatch.delenv("PMM_SEED")
+        assert np.array_equal(got[0], want[0]), metric
+        assert np.array_equal(got[1], want[1]), metric
+        check_topk(got[0], got[1], truth_scores(q, c, metric), metric != "euclidean",
+                   label=f"seeded k={k} {metric}")
