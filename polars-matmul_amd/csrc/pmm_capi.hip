@@ -511,8 +511,8 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     if (metric != kMetricDot) {
       const int sq = metric == kMetricEuclidean;
       Timed t("norms_f32", s);
-      HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
-      if (!c_norms) HIP_TRY(launch_norms_f32(c, n, d, ldc, sq, cn, cn + n, s));
+      if (c_norms) HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
+      else HIP_TRY(launch_norms_pair_f32(q, m, ldq, qn, c, n, ldc, cn, cn + n, d, sq, s));
     }
     FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
     if (seed) {

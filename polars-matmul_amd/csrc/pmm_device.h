@@ -202,11 +202,11 @@ __device__ __forceinline__ double sqrt_rn<double>(double x) { return __dsqrt_rn(
 
 // TI = stored element type (f32, f64, or bf16 for the bf16 compute path, whose
 // norms are those of the bf16-rounded rows, accumulated in f32).
+// 8 lanes per row; gt = the thread's index over this array's rows * 8.
 template <typename T, typename TI = T>
-__global__ __launch_bounds__(256) void norms_kernel(const TI *__restrict__ a, int64_t rows,
-                                                    int64_t d, int64_t ld, int squared,
-                                                    T *__restrict__ out, T *__restrict__ inv) {
-  const int64_t gt = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void norms_rows(const TI *__restrict__ a, int64_t rows, int64_t d,
+                                           int64_t ld, int squared, T *__restrict__ out,
+                                           T *__restrict__ inv, int64_t gt) {
   const int64_t row = gt >> 3;
   const int j = threadIdx.x & 7;
   const bool valid = row < rows;
@@ -240,6 +240,28 @@ __global__ __launch_bounds__(256) void norms_kernel(const TI *__restrict__ a, in
     // so 2*dot - factor over-estimates qsq - sq by more than its rounding.
     if (inv) inv[row] = squared ? v * (T)(1.0 - 0x1p-18) : ((v > (T)1e-6) ? (T)1 / v : (T)0);
   }
+}
+
+template <typename T, typename TI = T>
+__global__ __launch_bounds__(256) void norms_kernel(const TI *__restrict__ a, int64_t rows,
+                                                    int64_t d, int64_t ld, int squared,
+                                                    T *__restrict__ out, T *__restrict__ inv) {
+  norms_rows<T, TI>(a, rows, d, ld, squared, out, inv, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+}
+
+// Query and corpus norms in one launch: blocks [0, qblocks) take the query
+// rows, the rest the corpus rows (same arithmetic as two norms_kernel launches).
+template <typename T>
+__global__ __launch_bounds__(256) void norms_pair_kernel(const T *__restrict__ q, int64_t m, int64_t ldq,
+                                                         T *__restrict__ qout, const T *__restrict__ c,
+                                                         int64_t n, int64_t ldc, T *__restrict__ cout,
+                                                         T *__restrict__ cinv, int64_t d, int squared,
+                                                         unsigned qblocks) {
+  if (blockIdx.x < qblocks)
+    norms_rows<T, T>(q, m, d, ldq, squared, qout, nullptr, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
+  else
+    norms_rows<T, T>(c, n, d, ldc, squared, cout, cinv,
+                     (int64_t)(blockIdx.x - qblocks) * blockDim.x + threadIdx.x);
 }
 
 // ===========================================================================

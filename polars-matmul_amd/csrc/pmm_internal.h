@@ -81,6 +81,9 @@ struct RowSelArgs {
 };
 
 // ---- launchers (pmm_kernels.hip) ----
+hipError_t launch_norms_pair_f32(const float *q, int64_t m, int64_t ldq, float *qout, const float *c,
+                                 int64_t n, int64_t ldc, float *cout, float *cinv, int64_t d, int squared,
+                                 hipStream_t s);
 hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld, int squared,
                             float *out, float *inv, hipStream_t s);
 hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,

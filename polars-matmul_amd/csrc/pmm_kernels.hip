@@ -30,6 +30,14 @@ hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld,
   norms_kernel<float><<<grid, 256, 0, s>>>(a, rows, d, ld, squared, out, inv);
   return hipGetLastError();
 }
+hipError_t launch_norms_pair_f32(const float *q, int64_t m, int64_t ldq, float *qout, const float *c,
+                                 int64_t n, int64_t ldc, float *cout, float *cinv, int64_t d, int squared,
+                                 hipStream_t s) {
+  const unsigned gq = (unsigned)((m * 8 + 255) / 256), gc = (unsigned)((n * 8 + 255) / 256);
+  if (gq + gc == 0) return hipSuccess;
+  norms_pair_kernel<float><<<gq + gc, 256, 0, s>>>(q, m, ldq, qout, c, n, ldc, cout, cinv, d, squared, gq);
+  return hipGetLastError();
+}
 hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,
                             double *out, hipStream_t s) {
   if (rows <= 0) return hipSuccess;
