@@ -163,7 +163,8 @@ def measure_extra(name, steps, warmup, dev):
     el = time.perf_counter() - t0
     _native.timing_enable(False)
     kms, kn = _native.timing_read("gemm_bf16_topk" if bf16 else "gemm_f32_topk")
-    ach = 2.0 * M * N * D / (kms / kn / 1000.0) / 1e12 if kn else None
+    sms, sn = _native.timing_read("gemm_f32_seed")
+    ach =2.0 * M * N * D / (kms / kn / 1000.0) / 1e12 if kn else None
     out = {
         "config": {"workload": f"{M}x{N}x{D} {cdt} {metric} k={k} ({name})"},
         "dtype": cdt, "value": round(M * steps / el, 2), "unit": "queries/s",
@@ -171,7 +172,8 @@ def measure_extra(name, steps, warmup, dev):
         "roofline": {"bound": "mfma", "achieved": round(ach, 2) if ach else None,
                      "peak": MFMA_PEAK_TFLOPS[cdt], "unit": "TFLOP/s",
                      "frac": round(ach / MFMA_PEAK_TFLOPS[cdt], 4) if ach else None,
-                     "kernel_ms_avg": round(kms / kn, 3) if kn else None},
+                     "kernel_ms_avg": round(kms / kn, 3) if kn else None,
+                     "seed_ms_avg": round(sms / sn, 3) if sn else None},
     }
     del runner, ws, q, c
     torch.cuda.empty_cache()
@@ -254,6 +256,7 @@ def main():
     _native.timing_enable(False)
     kern_ms, kern_n = _native.timing_read("gemm_bf16_topk" if bf16 else "gemm_f32_topk")
     merge_ms, merge_n = _native.timing_read("merge_topk")
+    seed_ms, seed_n = _native.timing_read("gemm_f32_seed")
     shard_ms, shard_n = _native.timing_read("merge_shards")
     # algorithmic bytes of this rank's last merge pass (the reduction's HBM
     # roofline), read from the workspace after the timed region
@@ -297,7 +300,10 @@ def main():
         torch.cuda.empty_cache()
         extra = {}
         for name in [x for x in args.extra.split(",") if x and x not in (args.config, "none")]:
-            extra[name] = measure_extra(name, args.steps, args.warmup, dev)
+            M_, N_, D_ = CONFIGS[name][:3]
+            small = M_ * N_ * D_ < 10**11  # sub-millisecond steps: time more of them
+            extra[name] = measure_extra(name, max(args.steps, 50) if small else args.steps,
+                                        max(args.warmup, 3) if small else args.warmup, dev)
             log(f"extra {name}: {extra[name]}")
 
     if rank != 0:
@@ -323,6 +329,9 @@ def main():
         "flops_per_launch": flops_launch,
         "merge_ms_avg": round(merge_ms / merge_n, 3) if merge_n else None,
         "shard_merge_ms_avg": round(shard_ms / shard_n, 3) if shard_n else None,
+        # threshold-seeding pass (small problems only): its own
+        # gemm_f32_kernel launch, not in kernel_ms_avg, counted in ms_per_step
+        "seed_ms_avg": round(seed_ms / seed_n, 3) if seed_n else None,
     }
     reduction = None
     if merge_n and merge_bytes:
