@@ -3,30 +3,38 @@
 
 Workload (BASELINE.json configs[2], the config its metric is quoted on; it fits
 one GPU): 100,000 queries x 1,000,000 corpus rows x 768 dims, f32, cosine,
-k = 100.  Synthetic N(0,1) f32 embeddings generated on device (torch.randn,
-seeded); inputs are resident in HBM before the timed region.
+k = 100.  Synthetic N(0,1) f32 embeddings generated on device in blocks of
+65,536 rows, each block from its own seeded torch generator (so every rank can
+generate any corpus row range, and the corpus is the same whatever the number
+of GPUs); inputs are resident in HBM before the timed region.
 
 One step = one full top-k pass of all M queries against the corpus:
   N = 1: fused GEMM + top-k (libpmm.so, pmm_topk_f32_device) over the corpus.
   N > 1: the corpus is row-sharded over the ranks (one process per GPU);
          each rank runs the fused top-k on its shard (global indices via
          index_base), rank 0 gathers the per-shard M x k lists over RCCL
-         (torch.distributed "nccl" = RCCL) and k-way merges them
-         (pmm_merge_topk_device).  Total work is fixed: "scaling": "strong".
+         (torch.distributed "nccl" = RCCL; one gather of a [2][M][k] block per
+         rank) and k-way merges them in place (pmm_merge_topk_strided_device).
+         Total work is fixed: "scaling": "strong".
 
-Run: python bench.py [--gpus N] [--steps K] [--warmup W]
-     (N > 1 under torch.distributed.run, one rank per GPU)
+Run: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c4|c5|c1|c2]
+  --gpus N > 1 without a torch.distributed launcher: this process starts N rank
+  processes itself (before touching the GPU) and exits with their status;
+  under torch.distributed.run, WORLD_SIZE must equal N.
 
 Prints ONE JSON line on rank 0 with the metric, the dominant kernel's roofline
 (achieved TFLOP/s from HIP events on its launch stream vs the 157.3 TFLOP/s
-f32 MFMA peak) and a CPU baseline (the oracle, a port of the reference's
-algorithm, on a bounded query sample on this host's cores).
+f32 MFMA peak) and CPU baselines (the oracle -- a port of the reference's
+algorithm -- on a bounded query sample on this host's cores; the reference's
+own benchmark size configs[0] in full under extra.c1).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,21 +44,96 @@ for _p in (os.path.join(ROOT, "polars-matmul_amd"), os.path.join(ROOT, "oracle")
         sys.path.insert(0, _p)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
 
 CONFIGS = {
     # name: (M, N, D, k, metric, compute dtype)
     "c3": (100_000, 1_000_000, 768, 100, "cosine", "f32"),
     "c4": (100_000, 1_000_000, 768, 100, "cosine", "bf16"),
+    "c5": (1_000_000, 10_000_000, 1024, 100, "cosine", "f32"),
     "c2": (1_000, 10_000, 256, 10, "dot", "f32"),
     "c1": (1_000, 10_000, 256, 10, "cosine", "f32"),
 }
+# the reference's own benchmark (examples/benchmark_topk.py:69-71): seed-42
+# NumPy randn inputs, generated on the host
+REF_INPUT_CONFIGS = ("c1", "c2")
 MFMA_PEAK_TFLOPS = {"f32": 157.3, "bf16": 2516.6}  # MI355X dense matrix peaks (MI355X_MICROARCH.md)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+QSEED, CSEED = 42, 1_000_003
+GEN_BLOCK = 65536
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+# ---------------------------------------------------------------------------
+# N-rank launcher (no GPU work in this process)
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int, argv, extra_env=None) -> int:
+    """Start n rank processes running this script with argv (one per GPU,
+    torchrun-style env: RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR/PORT) and
+    return the first non-zero exit status (0 if all succeed).  Children are
+    started fresh; this process never touches the GPU."""
+    env = dict(os.environ)
+    env.update({"WORLD_SIZE": str(n), "LOCAL_WORLD_SIZE": str(n), "MASTER_ADDR": "127.0.0.1",
+                "MASTER_PORT": str(_free_port())})
+    env.update(extra_env or {})
+    procs = []
+    for r in range(n):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=e))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            r = p.poll()
+            if r is None:
+                continue
+            pending.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                for o in pending:  # a failed rank would leave the others waiting in a collective
+                    o.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+# ---------------------------------------------------------------------------
+# synthetic inputs
+# ---------------------------------------------------------------------------
+def synth_rows(lo: int, hi: int, d: int, seed: int, dev):
+    """Rows [lo, hi) of an (unbounded) N(0,1) f32 matrix: block b of GEN_BLOCK
+    rows comes from torch.randn on a generator seeded with seed * 2^20 + b."""
+    import torch
+
+    out = torch.empty((hi - lo, d), dtype=torch.float32, device=dev)
+    if hi <= lo:
+        return out
+    g = torch.Generator(device=dev)
+    for b in range(lo // GEN_BLOCK, (hi - 1) // GEN_BLOCK + 1):
+        g.manual_seed(seed * (1 << 20) + b)
+        blk = torch.randn((GEN_BLOCK, d), generator=g, device=dev, dtype=torch.float32)
+        a0, a1 = max(lo, b * GEN_BLOCK), min(hi, (b + 1) * GEN_BLOCK)
+        out[a0 - lo:a1 - lo] = blk[a0 - b * GEN_BLOCK:a1 - b * GEN_BLOCK]
+        del blk
+    return out
+
+
+def ref_inputs(M, N, D):
+    """examples/benchmark_topk.py:69-71: np.random.seed(42); randn(M, D),
+    randn(N, D) in float64, cast to float32."""
+    np.random.seed(42)
+    q = np.random.randn(M, D).astype(np.float32)
+    c = np.random.randn(N, D).astype(np.float32)
+    return q, c
 
 
 def load_traffic(config: str):
@@ -66,46 +149,56 @@ def load_traffic(config: str):
         return None
 
 
-def cpu_baseline(q_dev, c_dev, k, metric, n_sample, threads):
-    """Time the oracle (reference structure: threaded GEMM, single-threaded
-    epilogue + per-row select) on the first n_sample queries vs the full
-    corpus; returns queries/sec."""
+# ---------------------------------------------------------------------------
+# CPU baselines (rank 0, N = 1 only)
+# ---------------------------------------------------------------------------
+def cpu_oracle_qps(q, c, k, metric, threads, reps=1, warm=0):
+    """The oracle (the reference's structure: threaded GEMM, single-threaded
+    epilogue + per-row select); median seconds of `reps` timed calls."""
     import oracle
 
-    q = q_dev[:n_sample].float().cpu().numpy()
-    c = c_dev.float().cpu().numpy()
     mid = oracle.metric_from_str(metric)
-    t0 = time.perf_counter()
-    oracle.topk(q, c, k, mid, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return n_sample / dt, dt
+    for _ in range(warm):
+        oracle.topk(q, c, k, mid, nthreads=threads)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        oracle.topk(q, c, k, mid, nthreads=threads)
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts))
+    return q.shape[0] / dt, dt
 
 
-def numpy_comparator_qps(q_dev, c_dev, k, n_sample):
+def numpy_comparator(q, c, k, reps=1, warm=0):
     """SURVEY 8d CPU baseline (2): the README's NumPy comparator
     (examples/benchmark_topk.py:14-33 in the reference) restated -- L2-normalise
     both sides, one BLAS GEMM, a per-row partial selection of k, then a sort
-    of those k -- on the first n_sample queries against the full corpus.
-    Cosine only; BLAS threads as the environment sets them."""
-    q = q_dev[:n_sample].float().cpu().numpy()
-    c = c_dev.float().cpu().numpy()
-    t0 = time.perf_counter()
-    qn = q / np.sqrt((q * q).sum(axis=1, keepdims=True))
-    cn = c / np.sqrt((c * c).sum(axis=1, keepdims=True))
-    sim = qn @ cn.T
-    cut = sim.shape[1] - k
-    part = np.argpartition(sim, cut, axis=1)[:, cut:]
-    vals = np.take_along_axis(sim, part, axis=1)
-    order = np.argsort(-vals, axis=1)
-    np.take_along_axis(part, order, axis=1)
-    dt = time.perf_counter() - t0
-    return n_sample / dt, dt
+    of those k.  Cosine only; BLAS threads as the environment sets them."""
+    def once():
+        qn = q / np.sqrt((q * q).sum(axis=1, keepdims=True))
+        cn = c / np.sqrt((c * c).sum(axis=1, keepdims=True))
+        sim = qn @ cn.T
+        cut = sim.shape[1] - k
+        part = np.argpartition(sim, cut, axis=1)[:, cut:]
+        vals = np.take_along_axis(sim, part, axis=1)
+        order = np.argsort(-vals, axis=1)
+        return np.take_along_axis(part, order, axis=1)
+
+    for _ in range(warm):
+        once()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        once()
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts))
+    return q.shape[0] / dt, dt
 
 
 def boundary_rates(q_dev, c_dev, k, metric_id, compute=0):
     """Host-boundary rates: host f32 buffers in, host idx/score
     out, through the C ABI, one call each (untimed by the contract's clock):
-      host_api: pmm_topk_f32 -- pads+uploads Q and C, computes, downloads;
+      host_api: pmm_topk_f32 -- pins, uploads Q and C, computes, downloads;
       cached_corpus: pmm_topk_f32_corpus -- corpus resident (uploaded once,
         as the Arrow-keyed cache does across map_batches calls), Q uploaded
         and results downloaded per call."""
@@ -115,6 +208,7 @@ def boundary_rates(q_dev, c_dev, k, metric_id, compute=0):
     ch = c_dev.cpu().numpy()
     M = qh.shape[0]
     out = {}
+    _native.topk_host(qh[:1024], ch[:4096], k, metric_id, compute=compute)  # first-call setup
     t0 = time.perf_counter()
     _native.topk_host(qh, ch, k, metric_id, compute=compute)
     out["host_api_qps"] = round(M / (time.perf_counter() - t0), 2)
@@ -131,53 +225,269 @@ def boundary_rates(q_dev, c_dev, k, metric_id, compute=0):
     return out
 
 
-def measure_extra(name, steps, warmup, dev):
-    """Secondary workload on this GPU (N = 1 runs only): the same timing as the
-    main line (inputs resident, K steps bracketed by synchronize), reported
-    under "extra" -- e.g. c4, BASELINE configs[3] (bf16 compute)."""
-    from polars_matmul import _native
-    from polars_matmul.sharded import ShardedTopK
+# ---------------------------------------------------------------------------
+# GPU measurement
+# ---------------------------------------------------------------------------
+def make_inputs(name, rank, world, dev):
+    """(q, corpus shard, shard row offset, shard rows) on this rank's device."""
+    import torch
 
     M, N, D, k, metric, cdt = CONFIGS[name]
-    mid = _native.metric_from_str(metric)
-    bf16 = cdt == "bf16"
-    g = torch.Generator(device=dev)
-    g.manual_seed(42)
-    q = torch.randn((M, D), generator=g, device=dev, dtype=torch.float32)
-    g.manual_seed(1_000_003)
-    c = torch.randn((N, D), generator=g, device=dev, dtype=torch.float32)
-    if bf16:
+    lo, hi = N * rank // world, N * (rank + 1) // world
+    if name in REF_INPUT_CONFIGS:
+        qh, ch = ref_inputs(M, N, D)
+        q = torch.from_numpy(qh).to(dev)
+        c = torch.from_numpy(ch[lo:hi].copy()).to(dev)
+    else:
+        q = synth_rows(0, M, D, QSEED, dev)
+        c = synth_rows(lo, hi, D, CSEED, dev)
+    if cdt == "bf16":
+        # BASELINE configs[3]: the same f32 embeddings rounded to bf16 (RNE) on
+        # device, resident before the timed region
         q, c = q.to(torch.bfloat16), c.to(torch.bfloat16)
-    compute = _native.COMPUTE_BF16 if bf16 else _native.COMPUTE_F32
-    ws = torch.empty(_native.workspace_bytes(M, N, D, k, mid, compute), dtype=torch.uint8, device=dev)
-    runner = ShardedTopK(q, c, 0, k, mid, workspace=ws)
+    return q, c, lo, hi - lo
+
+
+def timed_steps(runner, steps, warmup, dist):
+    import torch
+    from polars_matmul import _native
+
     for _ in range(warmup):
         runner.run()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
     torch.cuda.synchronize()
     _native.timing_reset()
     _native.timing_enable(True)
     t0 = time.perf_counter()
-    for _ in range(steps):
-        runner.run()
+    out = None
+    for i in range(steps):
+        out = runner.run()
+        if steps <= 50:
+            log(f"step {i + 1}/{steps} issued")
     torch.cuda.synchronize()
-    el = time.perf_counter() - t0
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
     _native.timing_enable(False)
-    kms, kn = _native.timing_read("gemm_bf16_topk" if bf16 else "gemm_f32_topk")
-    sms, sn = _native.timing_read("gemm_f32_seed")
-    ach =2.0 * M * N * D / (kms / kn / 1000.0) / 1e12 if kn else None
-    out = {
-        "config": {"workload": f"{M}x{N}x{D} {cdt} {metric} k={k} ({name})"},
-        "dtype": cdt, "value": round(M * steps / el, 2), "unit": "queries/s",
-        "ms_per_step": round(el / steps * 1000.0, 3), "steps": steps, "warmup": warmup,
-        "roofline": {"bound": "mfma", "achieved": round(ach, 2) if ach else None,
-                     "peak": MFMA_PEAK_TFLOPS[cdt], "unit": "TFLOP/s",
-                     "frac": round(ach / MFMA_PEAK_TFLOPS[cdt], 4) if ach else None,
-                     "kernel_ms_avg": round(kms / kn, 3) if kn else None,
-                     "seed_ms_avg": round(sms / sn, 3) if sn else None},
-    }
-    del runner, ws, q, c
-    torch.cuda.empty_cache()
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, out
+
+
+def kernel_stats(bf16):
+    from polars_matmul import _native
+
+    names = {"gemm": "gemm_bf16_topk" if bf16 else "gemm_f32_topk", "seed": "gemm_f32_seed",
+             "merge": "merge_topk", "shard_merge": "merge_shards", "norms": "norms_"}
+    out = {}
+    for key, nm in names.items():
+        ms, n = _native.timing_read(nm)
+        out[key] = (ms / n if n else None, n)
     return out
+
+
+def spot_check(q, c, lo, k, metric, out_i, out_s, rows, dist, world, rank):
+    """Correctness spot check on a few query rows (untimed): the f64 top-k of
+    every shard on its own rank (torch on device), gathered to rank 0 and
+    merged there, vs the returned global lists."""
+    import torch
+
+    dev = q.device
+    qd = q[rows].double()
+    cd = c.double()
+    s = qd @ cd.T
+    if metric == "cosine":
+        s = s / (qd.norm(dim=1, keepdim=True) * cd.norm(dim=1)[None, :])
+    largest = metric != "euclidean"
+    if metric == "euclidean":
+        s = torch.cdist(qd, cd)
+    kk = min(k, s.shape[1])
+    v, i = torch.topk(s, kk, dim=1, largest=largest)
+    loc = torch.full((len(rows), k), float("nan"), dtype=torch.float64, device=dev)
+    loc_i = torch.full((len(rows), k), -1, dtype=torch.int64, device=dev)
+    loc[:, :kk] = v
+    loc_i[:, :kk] = i + lo
+    if world > 1:
+        gv = [torch.empty_like(loc) for _ in range(world)] if rank == 0 else None
+        gi = [torch.empty_like(loc_i) for _ in range(world)] if rank == 0 else None
+        dist.gather(loc, gv, dst=0)
+        dist.gather(loc_i, gi, dst=0)
+        if rank != 0:
+            return None
+        allv, alli = torch.cat(gv, dim=1), torch.cat(gi, dim=1)
+        fill = float("-inf") if largest else float("inf")
+        allv = torch.where(torch.isnan(allv), torch.full_like(allv, fill), allv)
+        ref_v, pos = torch.topk(allv, k, dim=1, largest=largest)
+        ref_i = torch.gather(alli, 1, pos)
+    else:
+        ref_v, ref_i = loc, loc_i
+    got_i = out_i[rows].long()
+    got_s = out_s[rows].double()
+    kth = ref_v[:, -1:]
+    band = 1e-5 * kth.abs() + 1e-5
+    ok = (got_s >= kth - band) if largest else (got_s <= kth + band)
+    return {
+        "rows": int(len(rows)),
+        "valid_topk_frac": float(ok.float().mean().item()),
+        "exact_index_match_frac": float((got_i == ref_i).float().mean().item()),
+        "max_abs_score_err_vs_f64_topk": float((got_s - ref_v).abs().max().item()),
+    }
+
+
+def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8):
+    """One config's timed line (inputs resident, K steps bracketed by barrier
+    + synchronize, max over ranks).  Returns (fields, q, corpus shard)."""
+    import torch
+    from polars_matmul import _native
+    from polars_matmul.sharded import ShardedTopK
+
+    M, N, D, k, metric, cdt = CONFIGS[name]
+    bf16 = cdt == "bf16"
+    compute = _native.COMPUTE_BF16 if bf16 else _native.COMPUTE_F32
+    mid = _native.metric_from_str(metric)
+    q, c, lo, n_loc = make_inputs(name, rank, world, dev)
+    ws = torch.empty(_native.workspace_bytes(M, n_loc, D, k, mid, compute), dtype=torch.uint8, device=dev)
+    runner = ShardedTopK(q, c, lo, k, mid, workspace=ws)
+    torch.cuda.synchronize()
+    elapsed, (out_i, out_s) = timed_steps(runner, steps, warmup, dist)
+    ks = kernel_stats(bf16)
+    merge_bytes = _native.merge_bytes(ws.data_ptr(), M, n_loc, D, k, mid, compute) if ks["merge"][1] else None
+    check = None
+    if check_rows:
+        rows = torch.arange(0, M, max(1, M // check_rows), device=dev)[:check_rows]
+        check = spot_check(q, c, lo, k, metric, out_i, out_s, rows, dist, world, rank)
+    flops = 2.0 * M * n_loc * D
+    peak = MFMA_PEAK_TFLOPS[cdt]
+    gemm_ms, _ = ks["gemm"]
+    seed_ms, _ = ks["seed"]
+    all_gemm_ms = (gemm_ms or 0.0) + (seed_ms or 0.0)
+    ms_step = elapsed / steps * 1000.0
+    ach = flops / (all_gemm_ms / 1000.0) / 1e12 if gemm_ms else None
+    roof = {
+        "bound": "mfma",
+        "kernel": f"gemm_{cdt}_kernel (fused GEMM + metric + top-k)",
+        "achieved": round(ach, 2) if ach else None,
+        "peak": peak, "unit": "TFLOP/s",
+        "frac": round(ach / peak, 4) if ach else None,
+        "traffic": load_traffic(name) if world == 1 else None,
+        # per launch of the dominant kernel; a threshold-seeding pass
+        # (small problems only, DESIGN §3) is its own launch of the same
+        # kernel and is counted in "achieved"/"frac" too
+        "kernel_ms_avg": round(gemm_ms, 3) if gemm_ms else None,
+        "seed_ms_avg": round(seed_ms, 3) if seed_ms else None,
+        "flops_per_launch": flops,
+        # the whole step (norms, fills, seed, GEMM, merge, gather) against the peak
+        "step_frac": round(flops / (ms_step / 1000.0) / 1e12 / peak, 4),
+        "merge_ms_avg": round(ks["merge"][0], 3) if ks["merge"][0] else None,
+        "shard_merge_ms_avg": round(ks["shard_merge"][0], 3) if ks["shard_merge"][0] else None,
+        "norms_ms_avg": round(ks["norms"][0], 3) if ks["norms"][0] else None,
+    }
+    reduction = None
+    if ks["merge"][1] and merge_bytes:
+        mavg = ks["merge"][0] / 1000.0
+        gbs = merge_bytes / mavg / 1e9
+        reduction = {
+            "kernel": "merge_kernel (per-row merge of the split candidate buffers)",
+            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": merge_bytes,
+            "kernel_ms_avg": round(mavg * 1000.0, 3),
+        }
+        if ks["shard_merge"][1]:
+            # rank 0's k-way merge of the world x M x k (index, score) lists
+            sbytes = (world + 1) * M * k * 8
+            savg = ks["shard_merge"][0] / 1000.0
+            reduction["shard_merge"] = {"bytes_per_launch": sbytes, "kernel_ms_avg": round(savg * 1000.0, 3),
+                                        "achieved": round(sbytes / savg / 1e9, 1), "unit": "GB/s"}
+    fields = {
+        "config": {"workload": f"{M}x{N}x{D} {cdt} {metric} k={k} ({name})", "queries": M, "corpus": N,
+                   "dim": D, "k": k, "metric": metric,
+                   "parallelism": f"corpus-row-shard x{world}" if world > 1 else "single GPU"},
+        "dtype": cdt, "value": round(M * steps / elapsed, 2), "unit": "queries/s",
+        "ms_per_step": round(ms_step, 3), "steps": steps, "warmup": warmup,
+        "roofline": roof, "reduction_roofline": reduction, "check": check,
+    }
+    del runner, ws
+    return fields, q, c
+
+
+def cpu_selftest(args, rank, world):
+    """Launcher / gather / merge plumbing on CPU (gloo): a small synthetic
+    problem whose per-shard top-k and merge are plain torch on the host.  Used
+    by tests/test_bench_launcher.py; measures nothing."""
+    import torch
+    import torch.distributed as dist
+
+    from polars_matmul.sharded import ShardedTopK, shard_bounds
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    g = torch.Generator()
+    g.manual_seed(7)
+    M, N, D, k = 24, 300, 16, 10
+    q = torch.randn((M, D), generator=g)
+    c = torch.randn((N, D), generator=g)
+    lo, hi = shard_bounds(N, world, rank)
+
+    def local(qq, cc, kk, metric, base, oi, os_, ws):
+        v, i = torch.topk(qq @ cc.T, kk, dim=1)
+        oi.copy_(i.to(torch.int32) + base)
+        os_.copy_(v)
+
+    def merge(gathered, kk, metric, oi, os_):
+        ii = gathered[:, 0].permute(1, 0, 2).reshape(M, -1)
+        ss = gathered[:, 1].view(torch.float32).permute(1, 0, 2).reshape(M, -1)
+        v, pos = torch.topk(ss, kk, dim=1)
+        oi.copy_(torch.gather(ii, 1, pos))
+        os_.copy_(v)
+
+    st = ShardedTopK(q, c[lo:hi].contiguous(), lo, k, 1, local_topk=local, merge=merge)
+    oi, osc = st.run()
+    if rank == 0:
+        v, i = torch.topk(q @ c.T, k, dim=1)
+        ok = bool(torch.equal(oi.long(), i)) and bool(torch.allclose(osc, v))
+        print(json.dumps({"metric": "cpu selftest", "n_gpus": world, "ranks_ok": ok}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def extra_line(name, steps, warmup, dev, args):
+    """Secondary workload on this GPU (N = 1 runs only), reported under
+    "extra"; the reference-size configs also carry their CPU baselines timed
+    in full (configs[0] = c1: examples/benchmark_topk.py)."""
+    import torch
+
+    M, N, D = CONFIGS[name][:3]
+    small = M * N * D < 10**11  # sub-millisecond steps: time more of them
+    st, wu = (max(steps, 200), max(warmup, 10)) if small else (steps, warmup)
+    fields, q, c = measure(name, st, wu, 0, 1, None, dev, check_rows=8)
+    if name in REF_INPUT_CONFIGS and args.cpu_sample:
+        k, metric = CONFIGS[name][3], CONFIGS[name][4]
+        qh, ch = ref_inputs(M, N, D)
+        qps, dt = cpu_oracle_qps(qh, ch, k, metric, args.cpu_threads, reps=5, warm=2)
+        fields["cpu_baseline"] = {
+            "value": round(qps, 2), "unit": "queries/s", "cores": args.cpu_threads,
+            "host_nproc": os.cpu_count(), "kind": "port",
+            "sample": f"the full {M}x{N}x{D} {metric} k={k} workload (seed-42 inputs, "
+                      f"benchmark_topk.py:69-71), median of 5 after 2 warm-ups: {dt * 1000:.1f} ms; "
+                      "oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select)",
+        }
+        if metric == "cosine":
+            nq, ndt = numpy_comparator(qh, ch, k, reps=5, warm=2)
+            fields["cpu_baseline_numpy"] = {
+                "value": round(nq, 2), "unit": "queries/s",
+                "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                "host_nproc": os.cpu_count(), "kind": "port",
+                "sample": f"full workload, median of 5 after 2 warm-ups: {ndt * 1000:.1f} ms; the reference "
+                          "README's NumPy comparator (benchmark_topk.py:14-33)",
+            }
+    del q, c
+    torch.cuda.empty_cache()
+    return fields
 
 
 def main():
@@ -187,17 +497,30 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-sample", type=int, default=512,
-                    help="queries timed on the CPU baseline vs the full corpus (0 = skip)")
+                    help="queries timed on the CPU baseline vs the full corpus (0 = skip CPU baselines)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
     ap.add_argument("--extra", default="c4,c1,c2",
                     help="comma-separated secondary configs measured after the main line (N=1; 'none' = none)")
-    ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 torch top-k")
+    ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 top-k")
+    ap.add_argument("--cpu-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # this process only launches: no torch.cuda / HIP call happens here
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        sys.exit(2)
+    if args.cpu_selftest:
+        cpu_selftest(args, rank, world)
+        return
+
+    import torch
+
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -213,190 +536,78 @@ def main():
     _native.check(_native.lib().pmm_set_device(torch.cuda.current_device()))
 
     M, N, D, k, metric, cdt = CONFIGS[args.config]
-    bf16 = cdt == "bf16"
-    compute = _native.COMPUTE_BF16 if bf16 else _native.COMPUTE_F32
-    mid = _native.metric_from_str(metric)
-    lo = N * rank // world
-    hi = N * (rank + 1) // world
-    n_loc = hi - lo
-
-    g = torch.Generator(device=dev)
-    g.manual_seed(42)
-    q = torch.randn((M, D), generator=g, device=dev, dtype=torch.float32)
-    g.manual_seed(1_000_003 + rank)
-    c = torch.randn((n_loc, D), generator=g, device=dev, dtype=torch.float32)
-    if bf16:
-        # BASELINE configs[3]: the same f32 embeddings rounded to bf16 (RNE) on
-        # device, resident before the timed region
-        q, c = q.to(torch.bfloat16), c.to(torch.bfloat16)
-    ws_bytes = _native.workspace_bytes(M, n_loc, D, k, mid, compute)
-    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-    from polars_matmul.sharded import ShardedTopK
-
-    runner = ShardedTopK(q, c, lo, k, mid, workspace=ws)
-    torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        runner.run()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    _native.timing_reset()
-    _native.timing_enable(True)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        out_i, out_s = runner.run()
-        log(f"[rank {rank}] step {i + 1}/{args.steps} issued")
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    _native.timing_enable(False)
-    kern_ms, kern_n = _native.timing_read("gemm_bf16_topk" if bf16 else "gemm_f32_topk")
-    merge_ms, merge_n = _native.timing_read("merge_topk")
-    seed_ms, seed_n = _native.timing_read("gemm_f32_seed")
-    shard_ms, shard_n = _native.timing_read("merge_shards")
-    # algorithmic bytes of this rank's last merge pass (the reduction's HBM
-    # roofline), read from the workspace after the timed region
-    merge_bytes = _native.merge_bytes(ws.data_ptr(), M, n_loc, D, k, mid, compute) if merge_n else None
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # correctness spot check on a few rows (f64 torch on device; untimed)
-    check = None
-    if args.check and world == 1:
-        rows = torch.arange(0, M, max(1, M // args.check), device=dev)[: args.check]
-        qd = q[rows].double()
-        cd = c.double()
-        s = qd @ cd.T
-        if metric == "cosine":
-            s = s / (qd.norm(dim=1, keepdim=True) * cd.norm(dim=1)[None, :])
-        ref_s, ref_i = torch.topk(s, k, dim=1)
-        got_i = out_i[rows].long()
-        got_s = out_s[rows].double()
-        kth = ref_s[:, -1:]
-        band = 1e-5 * kth.abs() + 1e-5
-        in_set = torch.gather(s, 1, got_i) >= (kth - band)
-        check = {
-            "rows": int(rows.numel()),
-            "valid_topk_frac": float(in_set.float().mean().item()),
-            "exact_index_match_frac": float((got_i == ref_i).float().mean().item()),
-            "max_abs_score_err": float((got_s - torch.gather(s, 1, got_i)).abs().max().item()),
-        }
-        log(f"spot check: {check}")
+    fields, q, c = measure(args.config, args.steps, args.warmup, rank, world, dist, dev, args.check)
+    if fields["check"]:
+        log(f"spot check: {fields['check']}")
 
     boundary = None
-    if args.boundary and world == 1:
-        boundary = boundary_rates(q.float(), c.float(), k, mid, compute)
+    if args.boundary and world == 1 and args.config not in ("c5",):
+        boundary = boundary_rates(q.float(), c.float(), k, _native.metric_from_str(metric),
+                                  _native.COMPUTE_BF16 if cdt == "bf16" else _native.COMPUTE_F32)
         log(f"boundary: {boundary}")
+
+    cpu = cpu_np = None
+    if args.cpu_sample and world == 1 and rank == 0:
+        n_s = min(args.cpu_sample, M)
+        qh = q[:n_s].float().cpu().numpy()
+        ch = c.float().cpu().numpy()
+        # bf16: the oracle on the bf16-rounded rows (widened to f32, exact)
+        cpu_qps, cpu_dt = cpu_oracle_qps(qh, ch, k, metric, args.cpu_threads)
+        cpu = {
+            "value": round(cpu_qps, 2), "unit": "queries/s", "cores": args.cpu_threads,
+            "host_nproc": os.cpu_count(), "kind": "port",
+            "sample": f"first {n_s} queries x full {N}-row corpus, {D}d {cdt} {metric} k={k}; "
+                      f"oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select), {cpu_dt:.1f}s",
+        }
+        if metric == "cosine":
+            np_qps, np_dt = numpy_comparator(qh, ch, k)
+            cpu_np = {
+                "value": round(np_qps, 2), "unit": "queries/s",
+                "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                "host_nproc": os.cpu_count(), "kind": "port",
+                "sample": f"first {n_s} queries x full {N}-row corpus; the reference README's NumPy "
+                          f"comparator (normalise, BLAS GEMM, argpartition, argsort), {np_dt:.1f}s",
+            }
+        del ch
 
     extra = None
     if args.extra and world == 1:
-        del runner, ws
+        del q, c
         torch.cuda.empty_cache()
         extra = {}
         for name in [x for x in args.extra.split(",") if x and x not in (args.config, "none")]:
-            M_, N_, D_ = CONFIGS[name][:3]
-            small = M_ * N_ * D_ < 10**11  # sub-millisecond steps: time more of them
-            extra[name] = measure_extra(name, max(args.steps, 50) if small else args.steps,
-                                        max(args.warmup, 3) if small else args.warmup, dev)
-            log(f"extra {name}: {extra[name]}")
+            extra[name] = extra_line(name, args.steps, args.warmup, dev, args)
+            log(f"extra {name}: {json.dumps(extra[name])}")
 
     if rank != 0:
         if dist:
             dist.destroy_process_group()
         return
 
-    ms_per_step = elapsed / args.steps * 1000.0
-    qps = M * args.steps / elapsed
-    flops_launch = 2.0 * M * n_loc * D
-    avg_kern_s = (kern_ms / kern_n / 1000.0) if kern_n else None
-    achieved = flops_launch / avg_kern_s / 1e12 if avg_kern_s else None
-    peak = MFMA_PEAK_TFLOPS[cdt]
-    roofline = {
-        "bound": "mfma",
-        "kernel": f"gemm_{cdt}_kernel (fused GEMM + metric + top-k)",
-        "achieved": round(achieved, 2) if achieved else None,
-        "peak": peak,
-        "unit": "TFLOP/s",
-        "frac": round(achieved / peak, 4) if achieved else None,
-        "traffic": load_traffic(args.config),
-        "kernel_ms_avg": round(kern_ms / kern_n, 3) if kern_n else None,
-        "flops_per_launch": flops_launch,
-        "merge_ms_avg": round(merge_ms / merge_n, 3) if merge_n else None,
-        "shard_merge_ms_avg": round(shard_ms / shard_n, 3) if shard_n else None,
-        # threshold-seeding pass (small problems only): its own
-        # gemm_f32_kernel launch, not in kernel_ms_avg, counted in ms_per_step
-        "seed_ms_avg": round(seed_ms / seed_n, 3) if seed_n else None,
-    }
-    reduction = None
-    if merge_n and merge_bytes:
-        mavg = merge_ms / merge_n / 1000.0
-        gbs = merge_bytes / mavg / 1e9
-        reduction = {
-            "kernel": "merge_kernel (per-row merge of the split candidate buffers)",
-            "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "bytes_per_launch": merge_bytes,
-            "kernel_ms_avg": round(mavg * 1000.0, 3),
-        }
-        if shard_n:
-            # rank 0's k-way merge of the world x M x k (index, score) lists
-            sbytes = (world + 1) * M * k * 8
-            savg = shard_ms / shard_n / 1000.0
-            reduction["shard_merge"] = {"bytes_per_launch": sbytes, "kernel_ms_avg": round(savg * 1000.0, 3),
-                                        "achieved": round(sbytes / savg / 1e9, 1), "unit": "GB/s"}
-    cpu = None
-    if args.cpu_sample and world == 1:
-        n_s = min(args.cpu_sample, M)
-        # bf16: the oracle on the bf16-rounded rows (widened to f32, exact)
-        cpu_qps, cpu_dt = cpu_baseline(q, c, k, metric, n_s, args.cpu_threads)
-        cpu = {
-            "value": round(cpu_qps, 2),
-            "unit": "queries/s",
-            "cores": args.cpu_threads,
-            "kind": "port",
-            "sample": f"first {n_s} queries x full {N}-row corpus, {D}d {cdt} {metric} k={k}; "
-                      f"oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select), {cpu_dt:.1f}s",
-        }
-    cpu_np = None
-    if args.cpu_sample and world == 1 and metric == "cosine":
-        n_s = min(args.cpu_sample, M)
-        np_qps, np_dt = numpy_comparator_qps(q, c, k, n_s)
-        cpu_np = {
-            "value": round(np_qps, 2), "unit": "queries/s",
-            "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-            "kind": "port",
-            "sample": f"first {n_s} queries x full {N}-row corpus; the reference README's NumPy "
-                      f"comparator (normalise, BLAS GEMM, argpartition, argsort), {np_dt:.1f}s",
-        }
     line = {
         "metric": "cosine top-k queries/sec",
-        "value": round(qps, 2),
+        "value": fields["value"],
         "unit": "queries/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_step, 3),
+        "ms_per_step": fields["ms_per_step"],
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": cdt,
-        "data": "synthetic N(0,1) f32 embeddings generated on device (torch.randn, seeded)"
-                + (", rounded to bf16 on device" if bf16 else ""),
-        "config": {"workload": f"{M}x{N}x{D} {cdt} {metric} k={k} ({args.config})", "queries": M,
-                   "corpus": N, "dim": D, "k": k, "metric": metric,
-                   "parallelism": f"corpus-row-shard x{world}" if world > 1 else "single GPU"},
-        "roofline": roofline,
-        "reduction_roofline": reduction,
+        "data": ("synthetic N(0,1) f32 embeddings generated on device (torch.randn, one seeded generator "
+                 "per 65,536-row block)" if args.config not in REF_INPUT_CONFIGS else
+                 "seed-42 NumPy randn inputs (examples/benchmark_topk.py:69-71)")
+                + (", rounded to bf16 on device" if cdt == "bf16" else ""),
+        "config": fields["config"],
+        "roofline": fields["roofline"],
+        "reduction_roofline": fields["reduction_roofline"],
         "cpu_baseline": cpu,
         "cpu_baseline_numpy": cpu_np,
         "boundary": boundary,
         "extra": extra,
-        "check": check,
+        "check": fields["check"],
     }
     print(json.dumps(line), flush=True)
     if dist:

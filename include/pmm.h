@@ -146,6 +146,18 @@ int pmm_topk_bf16_device(const uint16_t *q, int64_t ldq, int64_t m, const uint16
                          uint32_t index_base, uint32_t *out_idx, float *out_score,
                          void *workspace, size_t workspace_bytes, void *stream);
 
+/* Row norms over device rows, the first stage of the metric pipeline:
+ * replaces compute_norms_f32 / compute_squared_norms_f32
+ * (src/metrics.rs:382-393; f64: compute_norms / compute_squared_norms,
+ * :368-379).  out[r] = sqrt(row.row) (squared = 0, cosine) or row.row
+ * (squared = 1, euclidean), accumulated in ndarray's unrolled_dot order
+ * over exactly d elements with no FMA contraction -- the values the fused
+ * top-k kernels use.  a has `rows` rows of stride ld elements (ld >= d). */
+int pmm_norms_f32_device(const float *a, int64_t ld, int64_t rows, int64_t d, int squared,
+                         float *out, void *stream);
+int pmm_norms_f64_device(const double *a, int64_t ld, int64_t rows, int64_t d, int squared,
+                         double *out, void *stream);
+
 /* k-way merge of per-shard top-k lists: idx/score are [m][lists][k_in] (each
  * list best-first, as pmm_topk_f32_device writes them; idx 0xFFFFFFFF marks
  * an empty slot).  Writes the best k_out of each row to out_idx/out_score
@@ -155,6 +167,18 @@ int pmm_topk_bf16_device(const uint16_t *q, int64_t ldq, int64_t m, const uint16
 int pmm_merge_topk_device(const uint32_t *idx, const float *score, int64_t m, int64_t lists,
                           int64_t k_in, int64_t k_out, int metric, uint32_t *out_idx,
                           float *out_score, void *stream);
+
+/* The same merge over any list layout: entry i of list s of row r is
+ * idx[r * row_stride + s * list_stride + i] (and the same offset in score).
+ * pmm_merge_topk_device is (lists * k_in, k_in).  The sharded path gathers
+ * each rank's [idx plane | score plane] (2 x m x k_in 32-bit words) straight
+ * into a [ranks][2][m][k_in] buffer with ONE collective and merges it in
+ * place: idx = buffer, score = buffer + m * k_in, row_stride = k_in,
+ * list_stride = 2 * m * k_in (no re-layout copy). */
+int pmm_merge_topk_strided_device(const uint32_t *idx, const float *score, int64_t m,
+                                  int64_t lists, int64_t k_in, int64_t row_stride,
+                                  int64_t list_stride, int64_t k_out, int metric,
+                                  uint32_t *out_idx, float *out_score, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Device-resident corpus: upload a corpus once and run many top-k calls

@@ -13,6 +13,8 @@ Every function restates a reference function (paths into the reference tree):
 * ``select_topk``      -> src/topk.rs:6-75
 * ``topk``             -> src/matmul.rs:420-469 (k clipped to N, f32 scores widened to f64)
 * ``matmul``           -> src/metrics.rs:40-255 (dst = Q * C^T)
+* ``pair_scores``      -> the element S[i, idx[i, j]] of ``similarity`` (f32),
+                          without materialising S (full-size parity checks)
 """
 from __future__ import annotations
 
@@ -60,6 +62,7 @@ def lib():
         L.oracle_topk_f32.restype = i64
         L.oracle_topk_f64.argtypes = [vp, i64, vp, i64, i64, i64, i32, i32, vp, vp]
         L.oracle_topk_f64.restype = i64
+        L.oracle_pair_scores_f32.argtypes = [vp, i64, vp, i64, i64, i32, vp, i64, i32, vp]
         _lib = L
     return _lib
 
@@ -126,3 +129,18 @@ def topk(q: np.ndarray, c: np.ndarray, k: int, metric: int, nthreads: int = 0):
     fn = lib().oracle_topk_f32 if dt == np.float32 else lib().oracle_topk_f64
     fn(_p(q), m, _p(c), n, d, k, metric, nthreads, _p(idx), _p(sc))
     return idx, sc
+
+
+def pair_scores(q: np.ndarray, c: np.ndarray, idx: np.ndarray, metric: int, nthreads: int = 0) -> np.ndarray:
+    """f32 scores of the (row i, corpus row idx[i, j]) pairs, bit for bit the
+    values ``similarity(q, c, metric)[i, idx[i, j]]`` holds (NaN for an empty
+    slot, idx 0xFFFFFFFF)."""
+    q, c = _as(q, np.float32), _as(c, np.float32)
+    idx = np.ascontiguousarray(idx).view(np.uint32) if idx.dtype in (np.int32, np.uint32) else \
+        np.ascontiguousarray(idx, dtype=np.uint32)
+    m, k = idx.shape
+    assert q.shape[0] == m and q.shape[1] == c.shape[1]
+    out = np.empty((m, k), dtype=np.float32)
+    lib().oracle_pair_scores_f32(_p(q), m, _p(c), c.shape[0], q.shape[1], metric, _p(idx), k,
+                                 nthreads, _p(out))
+    return out

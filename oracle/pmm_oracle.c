@@ -415,3 +415,46 @@ int64_t oracle_topk_f64(const double *q, int64_t m, const double *c, int64_t n, 
     free(s);
     return k;
 }
+
+/* Exact score of given (query row, corpus row) pairs, element by element the
+ * value oracle_similarity_f32 would hold at S[i][idx[i][j]]: the same
+ * k-ordered fmaf chain (metrics.rs:204-255 as restated above), the same
+ * norms (metrics.rs:382-393) and epilogue (metrics.rs:314-365).  Used by the
+ * full-size parity tests to re-score every returned (row, index) without
+ * materialising the M x N matrix.  idx 0xFFFFFFFF (an empty slot) -> NaN. */
+void oracle_pair_scores_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d,
+                            int metric, const uint32_t *idx, int64_t k, int nthreads,
+                            float *out) {
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for num_threads(nthreads) schedule(dynamic, 16)
+#endif
+    for (int64_t i = 0; i < m; i++) {
+        const float *qr = q + i * d;
+        const int sq = metric == METRIC_EUCLIDEAN;
+        float qn = 0.0f;
+        if (metric != METRIC_DOT) {
+            qn = udot_f32(qr, qr, d);
+            if (!sq) qn = sqrtf(qn);
+        }
+        for (int64_t j = 0; j < k; j++) {
+            const uint32_t id = idx[i * k + j];
+            if ((int64_t)id >= n) {
+                out[i * k + j] = NAN;
+                continue;
+            }
+            const float *cr = c + (int64_t)id * d;
+            float acc = 0.0f;
+            for (int64_t kk = 0; kk < d; kk++) acc = fmaf(qr[kk], cr[kk], acc);
+            if (metric == METRIC_DOT) {
+                out[i * k + j] = acc;
+                continue;
+            }
+            float cn = udot_f32(cr, cr, d);
+            if (!sq) cn = sqrtf(cn);
+            float s = acc;
+            oracle_epilogue_f32(&s, 1, 1, metric, &qn, &cn);
+            out[i * k + j] = s;
+        }
+    }
+}

@@ -1079,12 +1079,43 @@ int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64
   return PMM_OK;
 }
 
+int pmm_norms_f32_device(const float *a, int64_t ld, int64_t rows, int64_t d, int squared,
+                         float *out, void *stream) {
+  if (rows < 0 || d < 0 || ld < d) return fail(PMM_ERR_ARG, "bad norm sizes (rows=%lld d=%lld ld=%lld)",
+                                                (long long)rows, (long long)d, (long long)ld);
+  if (rows == 0) return PMM_OK;
+  int dev, rc;
+  if ((rc = ensure_device(&dev))) return rc;
+  HIP_TRY(launch_norms_f32(a, rows, d, ld, squared ? 1 : 0, out, nullptr, (hipStream_t)stream));
+  return PMM_OK;
+}
+
+int pmm_norms_f64_device(const double *a, int64_t ld, int64_t rows, int64_t d, int squared,
+                         double *out, void *stream) {
+  if (rows < 0 || d < 0 || ld < d) return fail(PMM_ERR_ARG, "bad norm sizes (rows=%lld d=%lld ld=%lld)",
+                                                (long long)rows, (long long)d, (long long)ld);
+  if (rows == 0) return PMM_OK;
+  int dev, rc;
+  if ((rc = ensure_device(&dev))) return rc;
+  HIP_TRY(launch_norms_f64(a, rows, d, ld, squared ? 1 : 0, out, (hipStream_t)stream));
+  return PMM_OK;
+}
+
 int pmm_merge_topk_device(const uint32_t *idx, const float *score, int64_t m, int64_t lists,
                           int64_t k_in, int64_t k_out, int metric, uint32_t *out_idx,
                           float *out_score, void *stream) {
+  return pmm_merge_topk_strided_device(idx, score, m, lists, k_in, lists * k_in, k_in, k_out, metric,
+                                       out_idx, out_score, stream);
+}
+
+int pmm_merge_topk_strided_device(const uint32_t *idx, const float *score, int64_t m,
+                                  int64_t lists, int64_t k_in, int64_t row_stride,
+                                  int64_t list_stride, int64_t k_out, int metric,
+                                  uint32_t *out_idx, float *out_score, void *stream) {
   int rc;
   if ((rc = check_metric(metric))) return rc;
-  if (m < 0 || lists < 1 || k_in < 0 || k_out < 0 || k_out > lists * k_in)
+  if (m < 0 || lists < 1 || k_in < 0 || k_out < 0 || k_out > lists * k_in || row_stride < 0 ||
+      list_stride < 0)
     return fail(PMM_ERR_ARG, "bad merge sizes (m=%lld lists=%lld k_in=%lld k_out=%lld)",
                 (long long)m, (long long)lists, (long long)k_in, (long long)k_out);
   if (k_out > kFusedMaxK) return fail(PMM_ERR_UNSUPPORTED, "merge k_out > %d", kFusedMaxK);
@@ -1096,6 +1127,8 @@ int pmm_merge_topk_device(const uint32_t *idx, const float *score, int64_t m, in
   ma.in_idx = idx;
   ma.in_score = score;
   ma.k_in = (int)k_in;
+  ma.row_stride = row_stride;
+  ma.list_stride = list_stride;
   ma.M = (int)m;
   ma.S = (int)lists;
   ma.k_out = (int)k_out;

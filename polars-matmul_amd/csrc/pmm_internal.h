@@ -58,10 +58,14 @@ struct MergeArgs {
   const unsigned *cnt;
   const unsigned long long *gthr;
   int capg;
-  // loader 1: gathered (idx, score) lists [M][S][k_in]
+  // loader 1: gathered (idx, score) lists; entry i of list s of row r is at
+  // in_idx[r * row_stride + s * list_stride + i] (same offsets in in_score):
+  // [M][S][k_in] is (S * k_in, k_in); the RCCL gather's [S][2][M][k_in]
+  // (idx plane, score plane per rank) is (k_in, 2 * M * k_in)
   const uint32_t *in_idx;
   const float *in_score;
   int k_in;
+  int64_t row_stride, list_stride;
   int M, S, k_out, P, metric;
   uint32_t index_base;
   uint32_t *out_idx;

@@ -66,9 +66,9 @@ hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld
 // invariant (the step advances only the scalar soffset).  The 16-byte chunks
 // of every 128-byte row are XOR-swizzled on the SOURCE address (chunk ^
 // ((row>>1)&7)) so the ds_read_b128 fragment reads hit 16 distinct bank slots.
-// Lane (r = lane&31, h = lane>>5) covers k = 16h..16h+15 of the step, so MFMA
-// substep s pairs k = s and k = 16+s (the dot product is order-free; f32
-// rounding differs from faer's order only within the stated tolerance).
+// Fragments are fed in natural K order (substep t pairs k = 2t and 2t+1, see
+// the K loop), so each output is the k-ordered fmaf chain of the oracle
+// bit for bit (v_mfma_f32_32x32x2_f32 is an exact f32 FMA chain).
 // ===========================================================================
 template <int NB, int NW>
 struct GemmShape {
@@ -230,13 +230,44 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         const char *st = smem + buf * G::STAGE;
 #pragma unroll
         for (int qd = 0; qd < 4; qd++) {
+#ifdef PMM_F32_PERMUTED_K
+          // (A/B build only) lane half h covers k = 16h..16h+15: substep j of
+          // group qd pairs k = 4qd+j with 16+4qd+j
           const int co = 16 * ((4 * h + qd) ^ swz);
           const f32x4 av = *(const f32x4 *)(st + a_rd + co);
           f32x4 b[NB];
 #pragma unroll
           for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
+          constexpr int jord[4] = {0, 1, 2, 3};
+#else
+          // Natural K order: each f32 MFMA substep pairs k = 2t (lanes 0-31)
+          // with k = 2t+1 (lanes 32-63), so every output element is the
+          // k-ordered fmaf chain of the oracle (pmm_oracle.c oracle_gemm_f32)
+          // bit for bit.  Half h reads chunk 2qd+h (k = 8qd+4h..+3) with one
+          // ds_read_b128; two v_permlane32_swap per chunk then trade the
+          // lower half's odd k for the upper half's even k, leaving
+          // regs {0,2,1,3} = k pairs (8qd,+1) (8qd+2,+3) (8qd+4,+5) (8qd+6,+7).
+          const int co = 16 * ((2 * qd + h) ^ swz);
+          f32x4 av = *(const f32x4 *)(st + a_rd + co);
+          f32x4 b[NB];
 #pragma unroll
-          for (int j = 0; j < 4; j++) {
+          for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
+          auto kpair = [](f32x4 &x) __attribute__((always_inline)) {
+            auto r0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[0]), __float_as_uint(x[1]), false, false);
+            auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[2]), __float_as_uint(x[3]), false, false);
+            x[0] = __uint_as_float(r0[0]);
+            x[1] = __uint_as_float(r0[1]);
+            x[2] = __uint_as_float(r1[0]);
+            x[3] = __uint_as_float(r1[1]);
+          };
+          kpair(av);
+#pragma unroll
+          for (int c = 0; c < NB; c++) kpair(b[c]);
+          constexpr int jord[4] = {0, 2, 1, 3};
+#endif
+#pragma unroll
+          for (int jj = 0; jj < 4; jj++) {
+            const int j = jord[jj];
 #pragma unroll
             for (int c = 0; c < NB; c++)
               acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], b[c][j], acc[c], 0, 0, 0);
@@ -462,10 +493,10 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   int cnt = 0;
   // candidate i of list s as a composite key (0 = empty)
   auto load_x = [&](int s, int i) __attribute__((always_inline)) -> u64 {
-    const int64_t seg = (int64_t)row * a.S + s;
-    if (LOADER == 0) return a.cand[seg * a.capg + i];
-    const uint32_t id = a.in_idx[seg * a.k_in + i];
-    const float sc = a.in_score[seg * a.k_in + i];
+    if (LOADER == 0) return a.cand[((int64_t)row * a.S + s) * a.capg + i];
+    const int64_t off = (int64_t)row * a.row_stride + (int64_t)s * a.list_stride + i;
+    const uint32_t id = a.in_idx[off];
+    const float sc = a.in_score[off];
     return id != 0xFFFFFFFFu ? ((u64)okey32(a.metric == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~id)
                              : 0ull;
   };

@@ -51,6 +51,9 @@ EXPORTED_SYMBOLS = (
     "pmm_topk_f32_device",
     "pmm_topk_bf16_device",
     "pmm_merge_topk_device",
+    "pmm_merge_topk_strided_device",
+    "pmm_norms_f32_device",
+    "pmm_norms_f64_device",
     "pmm_corpus_create_f32",
     "pmm_corpus_destroy",
     "pmm_corpus_info",
@@ -104,6 +107,10 @@ _SIGS = {
         [_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _u32, _vp, _vp, _vp, _sz, _vp], _i32
     ),
     "pmm_merge_topk_device": ([_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp], _i32),
+    "pmm_merge_topk_strided_device": (
+        [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp], _i32),
+    "pmm_norms_f32_device": ([_vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
+    "pmm_norms_f64_device": ([_vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_corpus_create_f32": ([_vp, _i64, _i64, ctypes.POINTER(ctypes.c_void_p)], _i32),
     "pmm_corpus_destroy": ([_vp], _i32),
     "pmm_corpus_info": (
@@ -213,6 +220,22 @@ def merge_device(idx_ptr: int, score_ptr: int, m: int, lists: int, k_in: int, k_
                  metric: int, out_idx_ptr: int, out_score_ptr: int, stream: int = 0) -> None:
     check(_lib.pmm_merge_topk_device(idx_ptr, score_ptr, m, lists, k_in, k_out, metric,
                                      out_idx_ptr, out_score_ptr, stream or None))
+
+
+def merge_strided_device(idx_ptr: int, score_ptr: int, m: int, lists: int, k_in: int,
+                         row_stride: int, list_stride: int, k_out: int, metric: int,
+                         out_idx_ptr: int, out_score_ptr: int, stream: int = 0) -> None:
+    check(_lib.pmm_merge_topk_strided_device(idx_ptr, score_ptr, m, lists, k_in, row_stride,
+                                             list_stride, k_out, metric, out_idx_ptr,
+                                             out_score_ptr, stream or None))
+
+
+def norms_device(a_ptr: int, ld: int, rows: int, d: int, squared: bool, out_ptr: int, *,
+                 f64: bool = False, stream: int = 0) -> None:
+    """Row norms (or squared norms) of device rows in the reference's order
+    (pmm_norms_f32_device / pmm_norms_f64_device)."""
+    fn = _lib.pmm_norms_f64_device if f64 else _lib.pmm_norms_f32_device
+    check(fn(a_ptr, ld, rows, d, 1 if squared else 0, out_ptr, stream or None))
 
 
 def workspace_bytes(m: int, n: int, d: int, k: int, metric: int, compute: int = COMPUTE_F32) -> int:

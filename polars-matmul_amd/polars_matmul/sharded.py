@@ -4,8 +4,9 @@ One process per GPU (``torch.distributed``; backend "nccl" is RCCL on ROCm).
 Every rank holds the full query block and a contiguous slice of the corpus
 rows; it runs the fused top-k on its slice with ``index_base`` = the slice's
 first global row, so its list already carries global corpus indices.  Rank 0
-gathers the per-rank ``M x k`` (index, score) lists over RCCL (xGMI) and
-k-way merges them.  The gather is the path's only exchange step; there is no
+gathers the per-rank ``M x k`` (index, score) lists over RCCL (xGMI) -- one
+collective, both planes of every rank landing in one ``[world][2][M][k]``
+buffer -- and k-way merges them in place.  The gather is the path's only exchange step; there is no
 collective on the GEMM itself.
 
 The reference is single-process (no counterpart).  The local top-k and the
@@ -69,14 +70,17 @@ def _device_topk_bf16(q: torch.Tensor, c: torch.Tensor, k: int, metric: int, ind
                              stream=torch.cuda.current_stream(q.device).cuda_stream)
 
 
-def _device_merge(lists_i: torch.Tensor, lists_s: torch.Tensor, k: int, metric: int,
-                  out_i: torch.Tensor, out_s: torch.Tensor) -> None:
+def _device_merge(gathered: torch.Tensor, k: int, metric: int, out_i: torch.Tensor,
+                  out_s: torch.Tensor) -> None:
+    """k-way merge of the gathered [world][2][M][k_in] lists (per rank: an
+    index plane, then a score plane) in place, with no re-layout copy
+    (pmm_merge_topk_strided_device)."""
     from . import _native
 
-    m, r, kin = lists_i.shape
-    _native.merge_device(lists_i.data_ptr(), lists_s.data_ptr(), m, r, kin, k, metric,
-                         out_i.data_ptr(), out_s.data_ptr(),
-                         stream=torch.cuda.current_stream(lists_i.device).cuda_stream)
+    world, _, m, kin = gathered.shape
+    _native.merge_strided_device(gathered.data_ptr(), gathered[0, 1].data_ptr(), m, world, kin,
+                                 kin, 2 * m * kin, k, metric, out_i.data_ptr(), out_s.data_ptr(),
+                                 stream=torch.cuda.current_stream(gathered.device).cuda_stream)
 
 
 class ShardedTopK:
@@ -112,11 +116,15 @@ class ShardedTopK:
         self.workspace = workspace
         m = queries.shape[0]
         dev = queries.device
-        self.loc_i = torch.empty((m, self.k), dtype=torch.int32, device=dev)
-        self.loc_s = torch.empty((m, self.k), dtype=torch.float32, device=dev)
+        # this rank's list as one [2][M][k] block of 32-bit words (index plane,
+        # score plane), so ONE gather moves both into the root's
+        # [world][2][M][k] buffer, which the merge reads in place
+        self.loc = torch.empty((2, m, self.k), dtype=torch.int32, device=dev)
+        self.loc_i = self.loc[0]
+        self.loc_s = self.loc[1].view(torch.float32)
         if self.world > 1 and self.rank == 0:
-            self.gath_i = [torch.empty_like(self.loc_i) for _ in range(self.world)]
-            self.gath_s = [torch.empty_like(self.loc_s) for _ in range(self.world)]
+            self.gathered = torch.empty((self.world, 2, m, self.k), dtype=torch.int32, device=dev)
+            self._gather_list = list(self.gathered.unbind(0))
             self.out_i = torch.empty_like(self.loc_i)
             self.out_s = torch.empty_like(self.loc_s)
 
@@ -126,11 +134,8 @@ class ShardedTopK:
         if self.world == 1:
             return self.loc_i, self.loc_s
         root = self.rank == 0
-        dist.gather(self.loc_i, self.gath_i if root else None, dst=0, group=self.group)
-        dist.gather(self.loc_s, self.gath_s if root else None, dst=0, group=self.group)
+        dist.gather(self.loc, self._gather_list if root else None, dst=0, group=self.group)
         if not root:
             return self.loc_i, self.loc_s
-        lists_i = torch.stack(self.gath_i, dim=1).contiguous()  # [M][world][k]
-        lists_s = torch.stack(self.gath_s, dim=1).contiguous()
-        self.merge(lists_i, lists_s, self.k, self.metric, self.out_i, self.out_s)
+        self.merge(self.gathered, self.k, self.metric, self.out_i, self.out_s)
         return self.out_i, self.out_s

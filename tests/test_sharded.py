@@ -34,15 +34,17 @@ def _okey(v: np.ndarray) -> np.ndarray:
     return np.where(np.isnan(v), 0, k)
 
 
-def cpu_merge(lists_i, lists_s, k, metric, out_i, out_s):
+def cpu_merge(gathered, k, metric, out_i, out_s):
     """Restatement of the merge kernel's semantics (best-first, ties -> lower
-    index, empty slots skipped) used as the CPU stand-in."""
-    li = lists_i.numpy().view(np.uint32)
-    ls = lists_s.numpy()
-    m = li.shape[0]
+    index, empty slots skipped) over the gathered [world][2][M][k] layout
+    (per rank an index plane and a score plane), used as the CPU stand-in."""
+    g = gathered.numpy()
+    li = g[:, 0].view(np.uint32)  # [world][M][k]
+    ls = g[:, 1].view(np.float32)
+    m = li.shape[1]
     for r in range(m):
-        idx = li[r].reshape(-1)
-        sc = ls[r].reshape(-1)
+        idx = li[:, r].reshape(-1)
+        sc = ls[:, r].reshape(-1)
         keep = idx != 0xFFFFFFFF
         idx, sc = idx[keep], sc[keep]
         rank_v = -sc if metric == oracle.EUCLIDEAN else sc
