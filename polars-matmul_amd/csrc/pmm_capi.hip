@@ -62,23 +62,46 @@ struct TimingRec {
   hipEvent_t a, b;
 };
 
+// Per-thread, per-device scratch arena.  Host entry points use it on the
+// thread's own stream and synchronise before returning; device entry points
+// called with workspace = NULL use it on the CALLER's stream and return
+// without synchronising.  `ev` is recorded behind the last device-API use, and
+// a use on a different stream first waits for it, so two streams never work
+// in the same bytes at once.
+struct ArenaSlot {
+  void *p = nullptr;
+  size_t bytes = 0;
+  hipEvent_t ev = nullptr;
+  hipStream_t last = nullptr;
+  bool used = false;
+};
+
 struct ThreadCtx {
-  int device = -1;
+  int device = -1;                   // pmm_set_device's choice for host calls (-1: current)
   std::vector<hipStream_t> streams;  // per device, created lazily, never destroyed
-  std::vector<void *> arena;         // per device scratch arena
-  std::vector<size_t> arena_bytes;
+  std::vector<ArenaSlot> arena;      // per device
   bool timing = false;
   std::vector<TimingRec> recs;
 };
 thread_local ThreadCtx t_ctx;
 
-int ensure_device(int *dev_out) {
-  if (t_ctx.device < 0) {
-    int cur = 0;
-    HIP_TRY(hipGetDevice(&cur));
-    t_ctx.device = cur;
+// Restores the caller's current HIP device when a host entry point switched it.
+struct DevScope {
+  int prev = -1;
+  ~DevScope() {
+    if (prev >= 0) (void)hipSetDevice(prev);
   }
-  const int dev = t_ctx.device;
+};
+
+// Device-pointer entry points (scope == NULL) run on the caller's current
+// device and leave it alone.  Host entry points pass a scope: they run on
+// `want` (a corpus handle's device), else on pmm_set_device's choice for this
+// thread, else on the current device, and restore the current device on return.
+int ensure_device(int *dev_out, DevScope *scope = nullptr, int want = -1) {
+  int cur = 0;
+  HIP_TRY(hipGetDevice(&cur));
+  int dev = cur;
+  if (scope) dev = want >= 0 ? want : (t_ctx.device >= 0 ? t_ctx.device : cur);
   {
     std::lock_guard<std::mutex> lk(g_dev_mu);
     if ((int)g_dev.size() <= dev) g_dev.resize(dev + 1);
@@ -97,7 +120,10 @@ int ensure_device(int *dev_out) {
       return fail(PMM_ERR_NODEVICE,
                   "libpmm is built for gfx950 (MI355X); HIP device %d is %s", dev, di.arch.c_str());
   }
-  HIP_TRY(hipSetDevice(dev));
+  if (dev != cur) {
+    HIP_TRY(hipSetDevice(dev));
+    scope->prev = cur;
+  }
   *dev_out = dev;
   return PMM_OK;
 }
@@ -109,25 +135,36 @@ int thread_stream(int dev, hipStream_t *s) {
   return PMM_OK;
 }
 
-// Grow-only per-thread, per-device scratch.  Growing waits for the stream so
-// in-flight work never sees its buffer freed.
+// Grow-only per-thread, per-device scratch (see ArenaSlot).  A use on another
+// stream than the last device-API use waits for that use's event; growing
+// waits for both, so in-flight work never sees its buffer freed.
 int arena(int dev, hipStream_t s, size_t bytes, void **p) {
-  if ((int)t_ctx.arena.size() <= dev) {
-    t_ctx.arena.resize(dev + 1, nullptr);
-    t_ctx.arena_bytes.resize(dev + 1, 0);
-  }
-  if (t_ctx.arena_bytes[dev] < bytes) {
-    if (t_ctx.arena[dev]) {
+  if ((int)t_ctx.arena.size() <= dev) t_ctx.arena.resize(dev + 1);
+  ArenaSlot &a = t_ctx.arena[dev];
+  if (!a.ev) HIP_TRY(hipEventCreateWithFlags(&a.ev, hipEventDisableTiming));
+  if (a.used && a.last != s) HIP_TRY(hipStreamWaitEvent(s, a.ev, 0));
+  if (a.bytes < bytes) {
+    if (a.p) {
+      if (a.used) HIP_TRY(hipEventSynchronize(a.ev));
       HIP_TRY(hipStreamSynchronize(s));
-      HIP_TRY(hipFree(t_ctx.arena[dev]));
-      t_ctx.arena[dev] = nullptr;
-      t_ctx.arena_bytes[dev] = 0;
+      HIP_TRY(hipFree(a.p));
+      a.p = nullptr;
+      a.bytes = 0;
     }
     size_t want = bytes + bytes / 8;
-    HIP_TRY(hipMalloc(&t_ctx.arena[dev], want));
-    t_ctx.arena_bytes[dev] = want;
+    HIP_TRY(hipMalloc(&a.p, want));
+    a.bytes = want;
   }
-  *p = t_ctx.arena[dev];
+  *p = a.p;
+  return PMM_OK;
+}
+
+// Marks the end of a device-API use of the arena on stream s (no host sync).
+int arena_record(int dev, hipStream_t s) {
+  ArenaSlot &a = t_ctx.arena[dev];
+  HIP_TRY(hipEventRecord(a.ev, s));
+  a.last = s;
+  a.used = true;
   return PMM_OK;
 }
 
@@ -475,6 +512,7 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
   if (k <= kFusedMaxK) {
     Plan p;
     plan_topk(m, n, dp, k, metric, cus, p);
+    const bool own = !ws;
     if (!ws) {
       int rc = arena(dev, s, p.total, &ws);
       if (rc) return rc;
@@ -522,11 +560,12 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
                             (unsigned long long *)(w + p.off_gthr)));
     }
     HIP_TRY(run_fused_f32(f, p, w, index_base, out_idx, out_score, "gemm_f32_topk", "merge_topk", s));
-    return PMM_OK;
+    return own ? arena_record(dev, s) : PMM_OK;
   }
   // k beyond the fused path: materialise score chunks, row-select them.
   MatPlan p;
   plan_materialise(m, n, k, 4, p);
+  const bool own = !ws;
   if (!ws) {
     int rc = arena(dev, s, p.total, &ws);
     if (rc) return rc;
@@ -566,7 +605,7 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
                                     (int)k, index_base, out_idx + r0 * k, out_score + r0 * k, s));
     }
   }
-  return PMM_OK;
+  return own ? arena_record(dev, s) : PMM_OK;
 }
 
 // bf16 compute path over device bf16 rows (row strides ldq / ldc >=
@@ -592,6 +631,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
   const int64_t dp = cdiv(d, kBf16DAlign) * kBf16DAlign;
   Plan p;
   plan_topk(m, n, dp, k, metric, cus, p, PMM_COMPUTE_BF16);
+  const bool own = !ws;
   if (!ws) {
     int rc = arena(dev, s, p.total, &ws);
     if (rc) return rc;
@@ -696,7 +736,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     Timed t("merge_topk", s);
     HIP_TRY(launch_merge(ma, 0, s));
   }
-  return PMM_OK;
+  return own ? arena_record(dev, s) : PMM_OK;
 }
 
 // Upload a host matrix rows x d into a device buffer with row stride dp,
@@ -872,7 +912,8 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
   if (compute == PMM_COMPUTE_BF16 && (rc = bf16_limits(d, k, n))) return rc;
   int dev;
-  if ((rc = ensure_device(&dev))) return rc;
+  DevScope scope;
+  if ((rc = ensure_device(&dev, &scope))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   if (compute == PMM_COMPUTE_BF16) {
@@ -957,7 +998,8 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
   int dev;
-  if ((rc = ensure_device(&dev))) return rc;
+  DevScope scope;
+  if ((rc = ensure_device(&dev, &scope))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   const int64_t dp = cdiv(d, 16) * 16;
@@ -1018,7 +1060,8 @@ int pmm_matmul_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t
   if (rc) return rc;
   if (m == 0 || n == 0) return PMM_OK;
   int dev;
-  if ((rc = ensure_device(&dev))) return rc;
+  DevScope scope;
+  if ((rc = ensure_device(&dev, &scope))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   const int64_t dp = cdiv(std::max<int64_t>(d, 1), 32) * 32;
@@ -1051,7 +1094,8 @@ int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64
   if (rc) return rc;
   if (m == 0 || n == 0) return PMM_OK;
   int dev;
-  if ((rc = ensure_device(&dev))) return rc;
+  DevScope scope;
+  if ((rc = ensure_device(&dev, &scope))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   const int64_t dp = cdiv(std::max<int64_t>(d, 1), 16) * 16;
@@ -1149,7 +1193,8 @@ int pmm_corpus_create_f32(const float *c, int64_t n, int64_t d, pmm_corpus **out
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
   int dev;
-  if ((rc = ensure_device(&dev))) return rc;
+  DevScope scope;
+  if ((rc = ensure_device(&dev, &scope))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   pmm_corpus *h = new pmm_corpus();
@@ -1207,9 +1252,9 @@ int pmm_topk_f32_corpus(const pmm_corpus *h, const float *q, int64_t m, int64_t 
   if (rc) return rc;
   if ((rc = check_metric(metric))) return rc;
   if (m == 0 || k == 0) return PMM_OK;
-  t_ctx.device = h->device;
   int dev;
-  if ((rc = ensure_device(&dev))) return rc;
+  DevScope scope;
+  if ((rc = ensure_device(&dev, &scope, h->device))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   const int64_t dp = h->dp;

@@ -195,8 +195,12 @@ __device__ __forceinline__ int next_pow2_dev(int x) {
 // ===========================================================================
 template <typename T>
 __device__ __forceinline__ T sqrt_rn(T x);
+// f32: __builtin_sqrtf (llvm.sqrt.f32, correctly rounded under hipcc's default
+// -fhip-fp32-correctly-rounded-divide-sqrt), as Rust's f32::sqrt.  NOT
+// __fsqrt_rn: without OCML_BASIC_ROUNDED_OPERATIONS that is the 1-ulp native
+// v_sqrt_f32 (it differed from the oracle on 15% of norms).
 template <>
-__device__ __forceinline__ float sqrt_rn<float>(float x) { return __fsqrt_rn(x); }
+__device__ __forceinline__ float sqrt_rn<float>(float x) { return __builtin_sqrtf(x); }
 template <>
 __device__ __forceinline__ double sqrt_rn<double>(double x) { return __dsqrt_rn(x); }
 
@@ -279,7 +283,7 @@ __device__ __forceinline__ float exact_score(float dot, float qv, float cv) {
   }
   const float sq = __fsub_rn(__fadd_rn(qv, cv), 2.0f * dot);
   const float mx = (sq > 0.0f) ? sq : 0.0f;
-  return __fsqrt_rn(mx);
+  return __builtin_sqrtf(mx);  // correctly rounded (see sqrt_rn)
 }
 template <int METRIC>
 __device__ __forceinline__ double exact_score_f64(double dot, double qv, double cv) {

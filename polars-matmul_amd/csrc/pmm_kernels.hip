@@ -107,6 +107,18 @@ size_t gemm_f32_lds_bytes(int variant, int mode, int capg) {
 }
 
 
+// K order of the f32 MFMA chain (A/B builds: -DPMM_F32_KORDER=n):
+//   2 (default): natural order; the LDS image of every 32-float K step is laid
+//      out by 4-byte LDS-DMA gathers so that lane half h's 16-byte fragment
+//      read of chunk 2qd+h holds k = 8qd+h, +2, +4, +6: MFMA substep t = 4qd+j
+//      pairs k = 2t (h = 0) with 2t+1 (h = 1) straight from one ds_read_b128;
+//   1: natural order from 16-byte DMA + two v_permlane32_swap per fragment;
+//   0: round-1 permuted order (substep pairs k = 4qd+j with 16+4qd+j; NOT
+//      bit-exact vs the oracle's k-ordered chain).
+#ifndef PMM_F32_KORDER
+#define PMM_F32_KORDER 2
+#endif
+
 template <int NB, int NW, int MODE, int METRIC>
 __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a) {
   using G = GemmShape<NB, NW>;
@@ -130,19 +142,43 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   constexpr bool XFORM = (METRIC != kMetricDot);
 
   // Loop-invariant per-lane byte offsets of this wave's LDS-DMA pieces.
-  uint32_t a_voff[4], b_voff[G::BPIECES];
+#if PMM_F32_KORDER == 2
+  // 4-byte gathers: piece i fills 256 LDS bytes = 2 rows; LDS dword p of a
+  // row (physical chunk p>>2, element j = p&3) holds logical chunk
+  // ch = (p>>2) ^ swizzle, i.e. k = 8*(ch>>1) + (ch&1) + 2j
+  constexpr int AP = 16, BP = 4 * G::BPIECES, PIECE = 256, DW = 4;
+  auto kofs = [&](int row) __attribute__((always_inline)) {
+    const int p = lane & 31;
+    const int ch = (p >> 2) ^ ((row >> 1) & 7);
+    return 4 * (8 * (ch >> 1) + (ch & 1) + 2 * (p & 3));
+  };
+  uint32_t a_voff[AP], b_voff[BP];
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
+  for (int i = 0; i < AP; i++) {
+    const int row = 2 * i + (lane >> 5);
+    a_voff[i] = (uint32_t)(row * a.ldq * 4 + kofs(row));
+  }
+#pragma unroll
+  for (int i = 0; i < BP; i++) {
+    const int col = 2 * (i * NW + wid) + (lane >> 5);
+    b_voff[i] = (uint32_t)(col * a.ldc * 4 + kofs(col));
+  }
+#else
+  constexpr int AP = 4, BP = G::BPIECES, PIECE = 1024, DW = 16;
+  uint32_t a_voff[AP], b_voff[BP];
+#pragma unroll
+  for (int i = 0; i < AP; i++) {
     const int row = 8 * i + (lane >> 3);
     const int ch = (lane & 7) ^ ((row >> 1) & 7);
     a_voff[i] = (uint32_t)(row * a.ldq * 4 + ch * 16);
   }
 #pragma unroll
-  for (int i = 0; i < G::BPIECES; i++) {
+  for (int i = 0; i < BP; i++) {
     const int col = (i * NW + wid) * 8 + (lane >> 3);
     const int ch = (lane & 7) ^ ((col >> 1) & 7);
     b_voff[i] = (uint32_t)(col * a.ldc * 4 + ch * 16);
   }
+#endif
   // Per-lane LDS read offsets (within a stage).
   const int swz = (r32 >> 1) & 7;
   const int a_rd = wid * 4096 + r32 * 128;
@@ -196,15 +232,23 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       const int col0 = tile * G::BN;
       return make_rsrc(a.c + (int64_t)col0 * a.ldc, (int64_t)min(G::BN, a.N - col0) * a.ldc * 4);
     };
-    auto stage = [&](int sb, __amdgpu_buffer_rsrc_t rb, int ks, int tile) {
+    // DMA pieces [lo, hi) of one K step (A pieces first, then B pieces)
+    auto stage = [&](int sb, __amdgpu_buffer_rsrc_t rb, int ks, int tile, int lo, int hi) {
       char *st = smem + sb * G::STAGE;
       const uint32_t soff = (uint32_t)ks * 128u;
+      // (the 16-byte form stays behind the dma16 helper: used directly in a
+      // kernel body, the gfx950-only size silently drops the kernel's host stub)
+      auto dma = [&](__amdgpu_buffer_rsrc_t r, char *dst, uint32_t voff) __attribute__((always_inline)) {
+        if (DW == 4) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void *)dst, 4, voff, soff, 0, 0);
+        else dma16(r, dst, voff, soff);
+      };
 #pragma unroll
-      for (int i = 0; i < 4; i++) dma16(ra, st + wid * 4096 + i * 1024, a_voff[i], soff);
+      for (int i = 0; i < AP; i++)
+        if (i >= lo && i < hi) dma(ra, st + wid * 4096 + i * PIECE, a_voff[i]);
 #pragma unroll
-      for (int i = 0; i < G::BPIECES; i++)
-        dma16(rb, st + G::A_BYTES + (i * NW + wid) * 1024, b_voff[i], soff);
-      if (MODE == 0 && XFORM && ks == 0 && wid == 0) {
+      for (int i = 0; i < BP; i++)
+        if (AP + i >= lo && AP + i < hi) dma(rb, st + G::A_BYTES + (i * NW + wid) * PIECE, b_voff[i]);
+      if (MODE == 0 && XFORM && ks == 0 && wid == 0 && lo == 0) {
         // the tile's pre-filter column factors ride with its first K step
         const int col0 = tile * G::BN;
         const __amdgpu_buffer_rsrc_t rc =
@@ -217,8 +261,18 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       }
     };
 
+    // the next K step's DMA goes out behind MFMA groups 0 .. NPART-1 of this
+    // one, TP / NPART pieces each (the natural-order image takes 4x the
+    // pieces of the 16-byte form; spread, they do not stall one group)
+    constexpr int TP = AP + BP;
+#ifdef PMM_F32_DMA_PARTS
+    constexpr int NPART = PMM_F32_DMA_PARTS;
+#else
+    constexpr int NPART = PMM_F32_KORDER == 2 ? 4 : 1;
+#endif
+    static_assert(TP % NPART == 0 && NPART <= 4, "DMA pieces split evenly over the MFMA groups");
     __amdgpu_buffer_rsrc_t rb = rsrc_b(t0);
-    stage(buf, rb, 0, t0);
+    stage(buf, rb, 0, t0, 0, TP);
     for (int tile = t0; tile < t1; tile++) {
       const bool last_tile = (tile + 1) >= t1;
       const __amdgpu_buffer_rsrc_t rbn = last_tile ? rb : rsrc_b(tile + 1);
@@ -230,7 +284,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         const char *st = smem + buf * G::STAGE;
 #pragma unroll
         for (int qd = 0; qd < 4; qd++) {
-#ifdef PMM_F32_PERMUTED_K
+#if PMM_F32_KORDER == 0
           // (A/B build only) lane half h covers k = 16h..16h+15: substep j of
           // group qd pairs k = 4qd+j with 16+4qd+j
           const int co = 16 * ((4 * h + qd) ^ swz);
@@ -238,7 +292,13 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           f32x4 b[NB];
 #pragma unroll
           for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
-          constexpr int jord[4] = {0, 1, 2, 3};
+#elif PMM_F32_KORDER == 2
+          // natural K order from the gathered LDS image (see the DMA offsets)
+          const int co = 16 * ((2 * qd + h) ^ swz);
+          const f32x4 av = *(const f32x4 *)(st + a_rd + co);
+          f32x4 b[NB];
+#pragma unroll
+          for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
 #else
           // Natural K order: each f32 MFMA substep pairs k = 2t (lanes 0-31)
           // with k = 2t+1 (lanes 32-63), so every output element is the
@@ -263,21 +323,22 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           kpair(av);
 #pragma unroll
           for (int c = 0; c < NB; c++) kpair(b[c]);
-          constexpr int jord[4] = {0, 2, 1, 3};
 #endif
 #pragma unroll
           for (int jj = 0; jj < 4; jj++) {
-            const int j = jord[jj];
+            // KORDER 1 reads the swapped registers in the order {0, 2, 1, 3}
+            const int j = PMM_F32_KORDER == 1 ? ((jj & 1) << 1) | (jj >> 1) : jj;
 #pragma unroll
             for (int c = 0; c < NB; c++)
               acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], b[c][j], acc[c], 0, 0, 0);
           }
-          if (qd == 0) {
-            // next step's LDS-DMA goes out behind the first MFMA group, so the
+          if (qd < NPART) {
+            // next step's LDS-DMA goes out behind the MFMA groups, so the
             // matrix pipe restarts right after the barrier
             __builtin_amdgcn_sched_barrier(0);
-            if (ks + 1 < KS) stage(buf ^ 1, rb, ks + 1, tile);
-            else if (!last_tile) stage(buf ^ 1, rbn, 0, tile + 1);
+            constexpr int PER = TP / NPART;
+            if (ks + 1 < KS) stage(buf ^ 1, rb, ks + 1, tile, qd * PER, qd * PER + PER);
+            else if (!last_tile) stage(buf ^ 1, rbn, 0, tile + 1, qd * PER, qd * PER + PER);
             __builtin_amdgcn_sched_barrier(0);
           }
         }
@@ -572,7 +633,9 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     if (x != 0ull) {
       id = (~(uint32_t)x) + (LOADER == 0 ? a.index_base : 0u);
       const float v = dekey32((uint32_t)(x >> 32));
-      sc = (a.metric == kMetricEuclidean) ? -v : v;
+      // euclidean keys rank -distance; 0 - v (not -v) returns a zero
+      // distance as +0.0, the oracle's sqrt(max(., 0))
+      sc = (a.metric == kMetricEuclidean) ? 0.0f - v : v;
     }
     a.out_idx[(int64_t)row * a.k_out + j] = id;
     a.out_score[(int64_t)row * a.k_out + j] = sc;
@@ -690,12 +753,12 @@ __device__ __forceinline__ T key_score(u64 k, int metric);
 template <>
 __device__ __forceinline__ float key_score<float>(u64 k, int metric) {
   const float v = dekey32((uint32_t)k);
-  return metric == kMetricEuclidean ? -v : v;
+  return metric == kMetricEuclidean ? 0.0f - v : v;  // +0.0 for a zero distance
 }
 template <>
 __device__ __forceinline__ double key_score<double>(u64 k, int metric) {
   const double v = dekey64(k);
-  return metric == kMetricEuclidean ? -v : v;
+  return metric == kMetricEuclidean ? 0.0 - v : v;
 }
 
 __device__ int ent_compact(Ent *scr, int cnt, int k, int P, Ent *Tv, bool *tfull, int lane) {

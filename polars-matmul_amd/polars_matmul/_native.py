@@ -11,7 +11,10 @@ RuntimeError with the library's message.
 from __future__ import annotations
 
 import ctypes
+import importlib.util
 import os
+import sys
+import threading
 
 import numpy as np
 
@@ -63,16 +66,31 @@ EXPORTED_SYMBOLS = (
     "pmm_timing_read",
 )
 
-if os.environ.get("PMM_NO_TORCH_PRELOAD") != "1":
-    # PyTorch-ROCm ships its own libamdhip64.so (same SONAME as /opt/rocm's).
-    # Whichever loads first wins the SONAME; if libpmm.so pulled in /opt/rocm's
-    # runtime before torch, torch would load a second HIP runtime and find no
-    # devices.  Loading torch first makes the whole process share one runtime,
-    # so torch tensors (device memory, streams) can be passed to the C ABI.
+def _preload_hip_runtime() -> None:
+    """PyTorch-ROCm ships its own libamdhip64.so (SONAME libamdhip64.so.7, as
+    /opt/rocm's).  Whichever is loaded first serves the whole process; if
+    libpmm.so pulled in /opt/rocm's runtime first, a later `import torch`
+    would run on a runtime it was not built against.  When torch is installed
+    (and not yet imported), its runtime library is loaded here by path --
+    without importing torch -- so libpmm.so and any later torch share it and
+    torch device pointers / streams can be passed to the C ABI."""
+    if os.environ.get("PMM_NO_TORCH_PRELOAD") == "1" or "torch" in sys.modules:
+        return
     try:
-        import torch  # noqa: F401
-    except Exception:
-        pass
+        spec = importlib.util.find_spec("torch")
+    except (ImportError, ValueError):
+        spec = None
+    if spec is None or not spec.origin:
+        return
+    hip = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(hip):
+        try:
+            ctypes.CDLL(hip, mode=ctypes.RTLD_GLOBAL)
+        except OSError:
+            pass
+
+
+_preload_hip_runtime()
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -266,15 +284,36 @@ def timing_read(kernel: str):
 
 
 class DeviceCorpus:
-    """An f32 corpus uploaded once to HBM with its norms (pmm_corpus_*)."""
+    """An f32 corpus uploaded once to HBM with its norms (pmm_corpus_*).
+
+    Reference-counted: ``acquire()`` / ``release()`` bracket a use (``topk``
+    does so itself); ``close()`` frees the device memory at once if no use is
+    in flight, else when the last one releases it -- a cache may evict a
+    handle while another thread is still searching it."""
 
     def __init__(self, c: np.ndarray):
         c = np.ascontiguousarray(c, dtype=np.float32)
         h = ctypes.c_void_p()
         check(_lib.pmm_corpus_create_f32(ptr(c), c.shape[0], c.shape[1], ctypes.byref(h)))
         self._h = h
+        self._lock = threading.Lock()
+        self._refs = 0
+        self._closing = False
         self.n, self.d = c.shape
         self.nbytes = c.nbytes
+
+    def acquire(self) -> "DeviceCorpus":
+        with self._lock:
+            if self._closing or not self._h:
+                raise RuntimeError("DeviceCorpus is closed")
+            self._refs += 1
+        return self
+
+    def release(self) -> None:
+        with self._lock:
+            self._refs -= 1
+            if self._refs == 0 and self._closing:
+                self._destroy()
 
     def topk(self, q: np.ndarray, k: int, metric: int):
         q = np.ascontiguousarray(q, dtype=np.float32)
@@ -283,13 +322,27 @@ class DeviceCorpus:
         m = q.shape[0]
         idx = np.empty((m, k), dtype=np.uint32)
         sc = np.empty((m, k), dtype=np.float32)
-        check(_lib.pmm_topk_f32_corpus(self._h, ptr(q), m, k, metric, ptr(idx), ptr(sc)))
+        self.acquire()
+        try:
+            check(_lib.pmm_topk_f32_corpus(self._h, ptr(q), m, k, metric, ptr(idx), ptr(sc)))
+        finally:
+            self.release()
         return idx, sc
 
-    def close(self) -> None:
+    def _destroy(self) -> None:  # with self._lock held
         if self._h:
             _lib.pmm_corpus_destroy(self._h)
             self._h = ctypes.c_void_p()
+
+    @property
+    def closed(self) -> bool:
+        return not self._h
+
+    def close(self) -> None:
+        with self._lock:
+            self._closing = True
+            if self._refs == 0:
+                self._destroy()
 
     def __del__(self):  # pragma: no cover - interpreter shutdown order
         try:

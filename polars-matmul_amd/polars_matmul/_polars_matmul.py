@@ -176,17 +176,23 @@ def _as_usize(k) -> int:
 
 # ---------------------------------------------------------------------------
 # Device-resident corpus cache.  Polars' map_batches may
-# call _topk repeatedly with the same corpus Series; Arrow buffers are
-# immutable, so an Arrow corpus is identified by its buffers' addresses and
-# sizes while the cache holds a reference to it (the addresses cannot be
-# reused meanwhile).  numpy inputs are mutable and are never cached.
-# PMM_CORPUS_CACHE=0 disables; PMM_CORPUS_CACHE_BYTES bounds HBM use.
+# call _topk repeatedly with the same corpus Series.  Only corpora that came
+# in as Polars Series or Arrow arrays are cached (their buffers persist across
+# calls; a Python list or numpy matrix is rebuilt or mutable, so it would only
+# fill the cache), identified by the buffers' addresses and sizes while the
+# cache holds a reference to the Arrow array (the addresses cannot be reused
+# meanwhile).  Arrow data is immutable by contract: a Series that shares
+# memory with a numpy array the caller then writes to in place gives stale
+# cached results -- clear_corpus_cache() or PMM_CORPUS_CACHE=0 in that case.
+# PMM_CORPUS_CACHE_BYTES bounds the HBM the cache holds (default 8 GiB).
+# Handles are reference-counted (DeviceCorpus.acquire/release), so evicting
+# or clearing never frees a corpus another thread is searching.
 # ---------------------------------------------------------------------------
 
 _cache_lock = threading.Lock()
 _cache: "collections.OrderedDict" = collections.OrderedDict()
 _CACHE_ON = os.environ.get("PMM_CORPUS_CACHE", "1") != "0"
-_CACHE_BYTES = int(os.environ.get("PMM_CORPUS_CACHE_BYTES", str(32 << 30)))
+_CACHE_BYTES = int(os.environ.get("PMM_CORPUS_CACHE_BYTES", str(8 << 30)))
 _CACHE_MIN_BYTES = 1 << 20  # small corpora are cheaper to upload than to cache
 
 
@@ -197,23 +203,28 @@ def _arrow_key(arr):
     return (str(arr.type), arr.offset, len(arr), bufs)
 
 
-def _cached_corpus(rv, c: np.ndarray):
+def _cached_corpus(original, rv, c: np.ndarray):
+    """An ACQUIRED DeviceCorpus for this corpus (the caller releases it), or
+    None when the corpus is not cacheable."""
+    if not (_is_polars_series(original) or isinstance(original, pa.Array)
+            or (isinstance(original, pa.ChunkedArray) and original.num_chunks == 1)):
+        return None
     key = _arrow_key(rv)
-    if not _CACHE_ON or key is None or c.nbytes < _CACHE_MIN_BYTES:
+    if not _CACHE_ON or key is None or c.nbytes < _CACHE_MIN_BYTES or c.nbytes > _CACHE_BYTES:
         return None
     with _cache_lock:
         hit = _cache.get(key)
         if hit is not None:
             _cache.move_to_end(key)
-            return hit[1]
+            return hit[1].acquire()
         dc = _native.DeviceCorpus(c)
         _cache[key] = (rv, dc)
         total = sum(v[1].nbytes for v in _cache.values())
         while total > _CACHE_BYTES and len(_cache) > 1:
             _, (_, old) = _cache.popitem(last=False)
             total -= old.nbytes
-            old.close()
-        return dc
+            old.close()  # freed now, or by its last in-flight user
+        return dc.acquire()
 
 
 def clear_corpus_cache() -> None:
@@ -274,9 +285,12 @@ def _topk(left, right, k, metric):
         idx = np.zeros((m, 0), dtype=np.uint32)
         sc = np.zeros((m, 0), dtype=np.float64)
     else:
-        dc = _cached_corpus(rv, c) if use_f32 else None
+        dc = _cached_corpus(right, rv, c) if use_f32 else None
         if dc is not None:
-            idx, sc = dc.topk(q, kk, metric_id)
+            try:
+                idx, sc = dc.topk(q, kk, metric_id)
+            finally:
+                dc.release()
         else:
             idx, sc = _native.topk_host(q, c, kk, metric_id)
         sc = sc.astype(np.float64, copy=False)  # src/matmul.rs:447 (f32 -> f64)

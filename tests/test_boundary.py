@@ -153,7 +153,11 @@ def test_extract_fixed_size_list_zero_copy_and_slice():
     arr = pa.FixedSizeListArray.from_arrays(pa.array(base), 4)
     m = _series_to_matrix(arr, np.float32)
     assert m.shape == (6, 4) and m.dtype == np.float32
-    assert np.shares_memory(m, np.asarray(arr.values)) or m.flags.c_contiguous
+    # src/matmul.rs:22-95: an Array[f32] of one chunk with no nulls is borrowed,
+    # not copied -- the matrix IS the Arrow child buffer
+    child = np.frombuffer(arr.values.buffers()[1], dtype=np.float32)
+    assert np.shares_memory(m, child)
+    assert m.ctypes.data == child.ctypes.data
     s = arr.slice(2, 3)
     assert _series_to_matrix(s, np.float32).tolist() == base.reshape(6, 4)[2:5].tolist()
     # f32 Array into the f64 path is cast
@@ -191,3 +195,41 @@ def test_pmm_namespace_placeholder_without_polars():
     except Exception:
         with pytest.raises(ImportError):
             polars_matmul.PmmNamespace(None)
+
+
+def test_import_does_not_import_torch():
+    # the product package needs no torch: only the HIP runtime library torch
+    # ships is preloaded by path (so torch, if imported later, shares it)
+    code = ("import sys; sys.path.insert(0, %r); import polars_matmul; "
+            "print('torch' in sys.modules)") % os.path.join(ROOT, "polars-matmul_amd")
+    out = subprocess.run([os.sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == "False"
+
+
+def test_device_corpus_refcount_defers_destroy(monkeypatch):
+    # a cache eviction must not free a corpus another thread is
+    # searching -- close() with a use in flight defers the destroy to release()
+    destroyed = []
+
+    class StubLib:
+        def pmm_corpus_destroy(self, h):
+            destroyed.append(h.value)
+            return 0
+
+    monkeypatch.setattr(_native, "_lib", StubLib())
+    dc = object.__new__(_native.DeviceCorpus)
+    import threading
+    dc._h = ctypes.c_void_p(1234)
+    dc._lock = threading.Lock()
+    dc._refs = 0
+    dc._closing = False
+    dc.acquire()
+    dc.close()
+    assert destroyed == [] and not dc.closed
+    with pytest.raises(RuntimeError):
+        dc.acquire()  # closing: no new users
+    dc.release()
+    assert destroyed == [1234] and dc.closed
+    dc.close()
+    assert destroyed == [1234]
