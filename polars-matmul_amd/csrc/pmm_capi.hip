@@ -79,6 +79,7 @@ struct ArenaSlot {
 struct ThreadCtx {
   int device = -1;                   // pmm_set_device's choice for host calls (-1: current)
   std::vector<hipStream_t> streams;  // per device, created lazily, never destroyed
+  std::vector<hipStream_t> copy_streams;  // per device: host uploads overlapped with compute
   std::vector<ArenaSlot> arena;      // per device
   bool timing = false;
   std::vector<TimingRec> recs;
@@ -128,10 +129,11 @@ int ensure_device(int *dev_out, DevScope *scope = nullptr, int want = -1) {
   return PMM_OK;
 }
 
-int thread_stream(int dev, hipStream_t *s) {
-  if ((int)t_ctx.streams.size() <= dev) t_ctx.streams.resize(dev + 1, nullptr);
-  if (!t_ctx.streams[dev]) HIP_TRY(hipStreamCreateWithFlags(&t_ctx.streams[dev], hipStreamNonBlocking));
-  *s = t_ctx.streams[dev];
+int thread_stream(int dev, hipStream_t *s, bool copy = false) {
+  std::vector<hipStream_t> &v = copy ? t_ctx.copy_streams : t_ctx.streams;
+  if ((int)v.size() <= dev) v.resize(dev + 1, nullptr);
+  if (!v[dev]) HIP_TRY(hipStreamCreateWithFlags(&v[dev], hipStreamNonBlocking));
+  *s = v[dev];
   return PMM_OK;
 }
 
@@ -393,9 +395,11 @@ int check_metric(int metric) {
 }
 
 // Store-mode GEMM over rows [0, rows) of q into out (ldo), raw or transformed.
+// counter_zeroed: the caller's fill already zeroed *counter (no extra launch).
 int gemm_store_f32(const float *q, int64_t ldq, int64_t rows, const float *c, int64_t ldc, int64_t n,
                    int64_t d, int metric, int store_metric, const float *qn, const float *cn,
-                   float *out, int64_t ldo, unsigned *counter, int cus, hipStream_t s) {
+                   float *out, int64_t ldo, unsigned *counter, int cus, hipStream_t s,
+                   const char *label = nullptr, bool counter_zeroed = false) {
   Plan p;
   p.variant = choose_variant(1, 0, rows, n, cus);
   plan_units(rows, n, gemm_f32_bm(p.variant), gemm_f32_bn(p.variant), cus, 0.1, 1 << 20, p);
@@ -421,8 +425,8 @@ int gemm_store_f32(const float *q, int64_t ldq, int64_t rows, const float *c, in
   a.out = out;
   a.ldo = ldo;
   a.store_metric = store_metric;
-  HIP_TRY(hipMemsetAsync(counter, 0, 4, s));
-  Timed t(store_metric ? "gemm_f32_scores" : "gemm_f32_matmul", s);
+  if (!counter_zeroed) HIP_TRY(hipMemsetAsync(counter, 0, 4, s));
+  Timed t(label ? label : (store_metric ? "gemm_f32_scores" : "gemm_f32_matmul"), s);
   HIP_TRY(launch_gemm_f32(a, p.variant, 1, p.grid, s));
   return PMM_OK;
 }
@@ -437,11 +441,9 @@ struct FusedF32 {
   int metric;
   const float *qn, *cn, *cpre;
 };
-// seed_gthr != NULL: the merge raises those thresholds instead of writing lists.
 hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t index_base,
                          uint32_t *out_idx, float *out_score, const char *gemm_label,
-                         const char *merge_label, hipStream_t s,
-                         unsigned long long *seed_gthr = nullptr) {
+                         const char *merge_label, hipStream_t s) {
   // whole query blocks first (see gemm_f32_kernel's unit decode)
   const int64_t units = p.qb_full ? p.qb_full + (int64_t)(p.QB - p.qb_full) * p.S : p.units;
   // the caller has zeroed [w, w + p.off_cand): counter, thresholds, counts
@@ -492,7 +494,6 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
   ma.index_base = index_base;
   ma.out_idx = out_idx;
   ma.out_score = out_score;
-  ma.seed_gthr = seed_gthr;
   Timed t(merge_label, s);
   return launch_merge(ma, 0, s);
 }
@@ -500,10 +501,16 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
 // c_norms: optional precomputed corpus norms for `metric` laid out as
 // [n norms | n pre-filter factors] (a pmm_corpus handle's cache); NULL =
 // compute them in this call.
+// keep_gthr: the workspace's shared per-row thresholds already hold a lower
+// bound of the rows' k-th best from earlier corpus chunks (see
+// topk_f32_host_chunked); they are kept instead of zeroed, so this chunk
+// only returns what can still enter the top-k (possibly fewer than k per row:
+// the rest are empty slots, which the chunk merge skips).
 int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c, int64_t ldc,
                          int64_t n, int64_t d, int64_t k, int metric, uint32_t index_base,
                          uint32_t *out_idx, float *out_score, void *ws, size_t ws_bytes,
-                         hipStream_t s, int dev, const float *c_norms = nullptr) {
+                         hipStream_t s, int dev, const float *c_norms = nullptr,
+                         bool keep_gthr = false) {
   // d is the logical dimension (norms follow ndarray's order over exactly d
   // elements); the GEMM runs over dp = roundup(d, 32), the rows being
   // zero-padded up to dp.
@@ -523,29 +530,31 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     float *qn = (float *)(w + p.off_qn), *cn = (float *)(w + p.off_cn);
     if (c_norms) cn = const_cast<float *>(c_norms);
     // Threshold seeding.  When every unit spans few corpus tiles (small
-    // problems: the reference's own benchmark size), a unit starts cold and
-    // most of its time goes to exact re-scores and compactions of the scores
-    // that fill its rows' buffers.  A first fused pass over the corpus's first
-    // ns rows gives each row the k-th best of that sample; since the same
-    // kernel computes the same f32 score for a (query, corpus row) pair in
-    // either pass, (its composite key - 1) is an exact lower bound of the
-    // row's final k-th best, and seeds the shared threshold.  The seed pass
-    // costs about as much at ns = 64 as at 1024 (c1: few workgroups, latency
-    // bound); 512 measured best by 1-2%.
+    // problems: the reference's own benchmark size), a unit starts cold: its
+    // first tile's scores nearly all survive the pre-filter and are re-scored
+    // exactly, appended and compacted, which took most of the kernel's time.
+    // Instead, the scores of the first ns corpus rows are computed first by
+    // the same MFMA main loop in store mode (the same natural-K-order chain
+    // and epilogue arithmetic, so bit-identical to the main pass's scores) into
+    // the still unused candidate buffers, and one wave per row selects the
+    // k-th best composite of that sample (seed_select_kernel): (that key - 1)
+    // is an exact lower bound of the row's final k-th best and seeds the
+    // shared threshold.  Two short launches instead of round 1's fused seed
+    // pass + merge (0.09 ms at c1).
     int64_t ns = std::min<int64_t>(n, next_pow2((int)std::max<int64_t>(512, 8 * k), 256));
     if (const char *ne = getenv("PMM_SEED_NS")) ns = std::min<int64_t>(n, std::max<int64_t>(atoll(ne), k));
     const char *se = getenv("PMM_SEED");
     bool seed = (se ? atoi(se) != 0 : ((int64_t)p.tps * gemm_f32_bn(p.variant) < 8192 && n >= 4 * ns)) &&
-                ns >= k && ns < n;
-    Plan ps;
-    if (seed) {
-      plan_topk(m, ns, dp, k, metric, cus, ps);
-      // carved from the main candidate buffers (unused until the main pass)
-      seed = ps.total <= p.off_qn - p.off_cand;
+                ns >= k && ns < n && ns <= kSeedMaxNs && !keep_gthr &&
+                (size_t)m * ns * 4 <= p.off_qn - p.off_cand;
+    // one fill zeroes the work counters (the main pass's and the seed store
+    // pass's), thresholds and buffer counts [0, off_cand)
+    if (keep_gthr) {
+      HIP_TRY(hipMemsetAsync(w + p.off_counter, 0, p.off_gthr - p.off_counter, s));
+      HIP_TRY(hipMemsetAsync(w + p.off_cnt, 0, p.off_cand - p.off_cnt, s));
+    } else {
+      HIP_TRY(hipMemsetAsync(w, 0, p.off_cand, s));
     }
-    // one fill zeroes the work counters, thresholds and buffer counts of the
-    // main pass [0, off_cand) and of the seed pass right behind it
-    HIP_TRY(hipMemsetAsync(w, 0, p.off_cand + (seed ? ps.off_cand : 0), s));
     if (metric != kMetricDot) {
       const int sq = metric == kMetricEuclidean;
       Timed t("norms_f32", s);
@@ -554,10 +563,13 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     }
     FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
     if (seed) {
-      FusedF32 fs = f;
-      fs.n = ns;
-      HIP_TRY(run_fused_f32(fs, ps, w + p.off_cand, 0u, nullptr, nullptr, "gemm_f32_seed", "merge_seed", s,
-                            (unsigned long long *)(w + p.off_gthr)));
+      float *sample = (float *)(w + p.off_cand);
+      int rc = gemm_store_f32(q, ldq, m, c, ldc, ns, dp, metric, 1, qn, cn, sample, ns,
+                              (unsigned *)(w + p.off_counter) + 16, cus, s, "gemm_f32_seed", true);
+      if (rc) return rc;
+      Timed t("seed_select", s);
+      HIP_TRY(launch_seed_select(sample, ns, (int)m, (int)ns, (int)k, metric,
+                                 (unsigned long long *)(w + p.off_gthr), s));
     }
     HIP_TRY(run_fused_f32(f, p, w, index_base, out_idx, out_score, "gemm_f32_topk", "merge_topk", s));
     return own ? arena_record(dev, s) : PMM_OK;
@@ -768,6 +780,94 @@ int validate_sizes(int64_t m, int64_t n, int64_t d, int64_t k, bool topk, bool a
   return PMM_OK;
 }
 
+// Host-buffer f32 top-k over a large corpus with the upload overlapped with
+// compute.  The corpus is cut into chunks: a small first one (uploaded, with
+// the queries, before any compute) and CHUNKS-1 equal ones.  Chunk i + 1 is
+// copied on the thread's copy stream while chunk i's fused top-k runs on the
+// compute stream; each chunk's list carries global indices (index_base) into
+// a [chunks][2][m][k] buffer (index plane, score plane), merged in place at
+// the end -- the sharded path's merge, on one device.  The shared per-row
+// thresholds carry from chunk to chunk (keep_gthr): a chunk's k-th composite
+// is a lower bound of the global k-th, so later chunks start pruned and the
+// result equals the one-launch result bit for bit.
+constexpr size_t kChunkedMinBytes = size_t(256) << 20;  // corpus bytes from which uploads overlap
+constexpr int kChunks = 4;
+
+int topk_f32_host_chunked(const float *q, int64_t m, const float *c, int64_t n, int64_t d, int64_t k,
+                          int metric, uint32_t *out_idx, float *out_score, int dev, hipStream_t s) {
+  const int64_t dp = cdiv(d, 32) * 32;
+  int64_t bnd[kChunks + 1];
+  bnd[0] = 0;
+  bnd[1] = std::max<int64_t>(k, n / 16);
+  for (int i = 2; i <= kChunks; i++) bnd[i] = bnd[1] + (n - bnd[1]) * (i - 1) / (kChunks - 1);
+  size_t ws_need = 0;
+  for (int i = 0; i < kChunks; i++)
+    ws_need = std::max(ws_need, pmm_topk_workspace_bytes(m, bnd[i + 1] - bnd[i], dp, k, metric, PMM_COMPUTE_F32));
+  const size_t lists = (size_t)kChunks * 2 * m * k * 4;
+  size_t off_q = 0, off_c = al256((size_t)m * dp * 4), off_l = off_c + al256((size_t)n * dp * 4);
+  size_t off_i = off_l + al256(lists), off_s = off_i + al256((size_t)m * k * 4);
+  size_t off_w = off_s + al256((size_t)m * k * 4);
+  hipStream_t cs;
+  int rc;
+  if ((rc = thread_stream(dev, &cs, true))) return rc;
+  void *base;
+  if ((rc = arena(dev, s, off_w + ws_need, &base))) return rc;
+  char *b = (char *)base;
+  uint32_t *li = (uint32_t *)(b + off_l);
+  hipEvent_t ev[kChunks + 1] = {};
+  auto cleanup = [&]() {
+    for (auto &e : ev)
+      if (e) (void)hipEventDestroy(e);
+  };
+  for (auto &e : ev)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      cleanup();
+      return fail(PMM_ERR_HIP, "hipEventCreate failed");
+    }
+  // the copy stream must not overwrite the arena before earlier compute on
+  // the compute stream is done with it
+  hipEvent_t ready = ev[kChunks];
+  HIP_TRY(hipEventRecord(ready, s));
+  HIP_TRY(hipStreamWaitEvent(cs, ready, 0));
+  if ((rc = upload_padded(b + off_q, q, m, d, dp, 4, cs))) return cleanup(), rc;
+  for (int i = 0; i < kChunks; i++) {
+    const int64_t lo = bnd[i], rows = bnd[i + 1] - bnd[i];
+    // a pageable copy returns once staged: chunk i + 1 is copied while the
+    // device computes chunk i
+    if ((rc = upload_padded(b + off_c + (size_t)lo * dp * 4, c + lo * d, rows, d, dp, 4, cs)))
+      return cleanup(), rc;
+    HIP_TRY(hipEventRecord(ev[i], cs));
+    HIP_TRY(hipStreamWaitEvent(s, ev[i], 0));
+    rc = topk_f32_device_impl((const float *)(b + off_q), dp, m, (const float *)(b + off_c) + lo * dp, dp,
+                              rows, d, k, metric, (uint32_t)lo, li + (size_t)i * 2 * m * k,
+                              (float *)(li + (size_t)i * 2 * m * k + (size_t)m * k), b + off_w, ws_need, s,
+                              dev, nullptr, i > 0);
+    if (rc) return cleanup(), rc;
+  }
+  MergeArgs ma{};
+  ma.in_idx = li;
+  ma.in_score = (const float *)(li + (size_t)m * k);
+  ma.k_in = (int)k;
+  ma.row_stride = k;
+  ma.list_stride = 2 * m * k;
+  ma.M = (int)m;
+  ma.S = kChunks;
+  ma.k_out = (int)k;
+  ma.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
+  ma.metric = metric;
+  ma.out_idx = (uint32_t *)(b + off_i);
+  ma.out_score = (float *)(b + off_s);
+  {
+    Timed t("merge_chunks", s);
+    HIP_TRY(launch_merge(ma, 1, s));
+  }
+  HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  cleanup();
+  return PMM_OK;
+}
+
 }  // namespace
 
 // Device-resident corpus (pmm_corpus_*): padded f32 rows in HBM plus the
@@ -941,6 +1041,11 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
     return PMM_OK;
   }
   const int64_t dp = cdiv(d, 32) * 32;
+  {
+    const char *ce = getenv("PMM_CHUNKED_UPLOAD");  // 0: one upload, then one launch
+    if (k <= kFusedMaxK && (size_t)n * dp * 4 >= kChunkedMinBytes && n >= 64 * k && !(ce && atoi(ce) == 0))
+      return topk_f32_host_chunked(q, m, c, n, d, k, metric, out_idx, out_score, dev, s);
+  }
   size_t ws_need = pmm_topk_workspace_bytes(m, n, dp, k, metric, compute);
   size_t off_q = 0, off_c = al256((size_t)m * dp * 4), off_i = off_c + al256((size_t)n * dp * 4);
   size_t off_s = off_i + al256((size_t)m * k * 4), off_w = off_s + al256((size_t)m * k * 4);

@@ -70,9 +70,6 @@ struct MergeArgs {
   uint32_t index_base;
   uint32_t *out_idx;
   float *out_score;
-  // threshold seeding (topk_f32_device_impl): instead of writing the lists,
-  // raise seed_gthr[row] to (the row's k-th composite key - 1)
-  unsigned long long *seed_gthr;
 };
 
 struct RowSelArgs {
@@ -100,6 +97,11 @@ int gemm_f32_bm(int variant);   // query rows per workgroup
 int gemm_f32_bn(int variant);   // corpus columns per tile
 size_t gemm_f32_lds_bytes(int variant, int mode, int capg);
 hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s);
+// Threshold seeding: gthr[row] = (k-th best composite of the row's ns
+// materialised scores S[row][0..ns)) - 1, one wave per row; ns <= kSeedMaxNs.
+constexpr int kSeedMaxNs = 1024;
+hipError_t launch_seed_select(const float *S, int64_t lds, int m, int ns, int k, int metric,
+                              unsigned long long *gthr, hipStream_t s);
 // ---- bf16 compute path (pmm_bf16.hip) ----
 // Fused top-k on bf16 operands: 128 query rows x 128 corpus columns per
 // workgroup tile, 4 waves (1 per SIMD), query rows register-resident.

@@ -112,6 +112,8 @@ size_t gemm_f32_lds_bytes(int variant, int mode, int capg) {
 //      out by 4-byte LDS-DMA gathers so that lane half h's 16-byte fragment
 //      read of chunk 2qd+h holds k = 8qd+h, +2, +4, +6: MFMA substep t = 4qd+j
 //      pairs k = 2t (h = 0) with 2t+1 (h = 1) straight from one ds_read_b128;
+//   3: natural order, corpus image gathered, query image by 16-byte DMA with
+//      two v_permlane32_swap per query fragment;
 //   1: natural order from 16-byte DMA + two v_permlane32_swap per fragment;
 //   0: round-1 permuted order (substep pairs k = 4qd+j with 16+4qd+j; NOT
 //      bit-exact vs the oracle's k-ordered chain).
@@ -142,11 +144,15 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   constexpr bool XFORM = (METRIC != kMetricDot);
 
   // Loop-invariant per-lane byte offsets of this wave's LDS-DMA pieces.
-#if PMM_F32_KORDER == 2
-  // 4-byte gathers: piece i fills 256 LDS bytes = 2 rows; LDS dword p of a
-  // row (physical chunk p>>2, element j = p&3) holds logical chunk
-  // ch = (p>>2) ^ swizzle, i.e. k = 8*(ch>>1) + (ch&1) + 2j
-  constexpr int AP = 16, BP = 4 * G::BPIECES, PIECE = 256, DW = 4;
+  // Gathered image (4-byte pieces of 256 LDS bytes = 2 rows): LDS dword p of
+  // a row (physical chunk p>>2, element j = p&3) holds logical chunk
+  // ch = (p>>2) ^ swizzle, i.e. k = 8*(ch>>1) + (ch&1) + 2j.  Plain image
+  // (16-byte pieces of 1 KiB = 8 rows): chunk ch of a row at ch ^ swizzle.
+  constexpr bool A_GATHER = PMM_F32_KORDER == 2;
+  constexpr bool B_GATHER = PMM_F32_KORDER == 2 || PMM_F32_KORDER == 3;
+  constexpr int AP = A_GATHER ? 16 : 4, APIECE = A_GATHER ? 256 : 1024, ADW = A_GATHER ? 4 : 16;
+  constexpr int BP = B_GATHER ? 4 * G::BPIECES : G::BPIECES, BPIECE = B_GATHER ? 256 : 1024,
+                BDW = B_GATHER ? 4 : 16;
   auto kofs = [&](int row) __attribute__((always_inline)) {
     const int p = lane & 31;
     const int ch = (p >> 2) ^ ((row >> 1) & 7);
@@ -155,30 +161,26 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   uint32_t a_voff[AP], b_voff[BP];
 #pragma unroll
   for (int i = 0; i < AP; i++) {
-    const int row = 2 * i + (lane >> 5);
-    a_voff[i] = (uint32_t)(row * a.ldq * 4 + kofs(row));
+    if (A_GATHER) {
+      const int row = 2 * i + (lane >> 5);
+      a_voff[i] = (uint32_t)(row * a.ldq * 4 + kofs(row));
+    } else {
+      const int row = 8 * i + (lane >> 3);
+      const int ch = (lane & 7) ^ ((row >> 1) & 7);
+      a_voff[i] = (uint32_t)(row * a.ldq * 4 + ch * 16);
+    }
   }
 #pragma unroll
   for (int i = 0; i < BP; i++) {
-    const int col = 2 * (i * NW + wid) + (lane >> 5);
-    b_voff[i] = (uint32_t)(col * a.ldc * 4 + kofs(col));
+    if (B_GATHER) {
+      const int col = 2 * (i * NW + wid) + (lane >> 5);
+      b_voff[i] = (uint32_t)(col * a.ldc * 4 + kofs(col));
+    } else {
+      const int col = (i * NW + wid) * 8 + (lane >> 3);
+      const int ch = (lane & 7) ^ ((col >> 1) & 7);
+      b_voff[i] = (uint32_t)(col * a.ldc * 4 + ch * 16);
+    }
   }
-#else
-  constexpr int AP = 4, BP = G::BPIECES, PIECE = 1024, DW = 16;
-  uint32_t a_voff[AP], b_voff[BP];
-#pragma unroll
-  for (int i = 0; i < AP; i++) {
-    const int row = 8 * i + (lane >> 3);
-    const int ch = (lane & 7) ^ ((row >> 1) & 7);
-    a_voff[i] = (uint32_t)(row * a.ldq * 4 + ch * 16);
-  }
-#pragma unroll
-  for (int i = 0; i < BP; i++) {
-    const int col = (i * NW + wid) * 8 + (lane >> 3);
-    const int ch = (lane & 7) ^ ((col >> 1) & 7);
-    b_voff[i] = (uint32_t)(col * a.ldc * 4 + ch * 16);
-  }
-#endif
   // Per-lane LDS read offsets (within a stage).
   const int swz = (r32 >> 1) & 7;
   const int a_rd = wid * 4096 + r32 * 128;
@@ -238,16 +240,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       const uint32_t soff = (uint32_t)ks * 128u;
       // (the 16-byte form stays behind the dma16 helper: used directly in a
       // kernel body, the gfx950-only size silently drops the kernel's host stub)
-      auto dma = [&](__amdgpu_buffer_rsrc_t r, char *dst, uint32_t voff) __attribute__((always_inline)) {
-        if (DW == 4) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void *)dst, 4, voff, soff, 0, 0);
+      auto dma = [&](__amdgpu_buffer_rsrc_t r, char *dst, uint32_t voff, int dw) __attribute__((always_inline)) {
+        if (dw == 4) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void *)dst, 4, voff, soff, 0, 0);
         else dma16(r, dst, voff, soff);
       };
 #pragma unroll
       for (int i = 0; i < AP; i++)
-        if (i >= lo && i < hi) dma(ra, st + wid * 4096 + i * PIECE, a_voff[i]);
+        if (i >= lo && i < hi) dma(ra, st + wid * 4096 + i * APIECE, a_voff[i], ADW);
 #pragma unroll
       for (int i = 0; i < BP; i++)
-        if (AP + i >= lo && AP + i < hi) dma(rb, st + G::A_BYTES + (i * NW + wid) * PIECE, b_voff[i]);
+        if (AP + i >= lo && AP + i < hi) dma(rb, st + G::A_BYTES + (i * NW + wid) * BPIECE, b_voff[i], BDW);
       if (MODE == 0 && XFORM && ks == 0 && wid == 0 && lo == 0) {
         // the tile's pre-filter column factors ride with its first K step
         const int col0 = tile * G::BN;
@@ -266,9 +268,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     // pieces of the 16-byte form; spread, they do not stall one group)
     constexpr int TP = AP + BP;
 #ifdef PMM_F32_DMA_PARTS
-    constexpr int NPART = PMM_F32_DMA_PARTS;
+    constexpr int NPART = PMM_F32_DMA_PARTS;  // (A/B: 4 measured 7% slower at c3)
 #else
-    constexpr int NPART = PMM_F32_KORDER == 2 ? 4 : 1;
+    constexpr int NPART = 1;
 #endif
     static_assert(TP % NPART == 0 && NPART <= 4, "DMA pieces split evenly over the MFMA groups");
     __amdgpu_buffer_rsrc_t rb = rsrc_b(t0);
@@ -284,34 +286,21 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         const char *st = smem + buf * G::STAGE;
 #pragma unroll
         for (int qd = 0; qd < 4; qd++) {
-#if PMM_F32_KORDER == 0
-          // (A/B build only) lane half h covers k = 16h..16h+15: substep j of
-          // group qd pairs k = 4qd+j with 16+4qd+j
-          const int co = 16 * ((4 * h + qd) ^ swz);
-          const f32x4 av = *(const f32x4 *)(st + a_rd + co);
-          f32x4 b[NB];
-#pragma unroll
-          for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
-#elif PMM_F32_KORDER == 2
-          // natural K order from the gathered LDS image (see the DMA offsets)
-          const int co = 16 * ((2 * qd + h) ^ swz);
-          const f32x4 av = *(const f32x4 *)(st + a_rd + co);
-          f32x4 b[NB];
-#pragma unroll
-          for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
-#else
-          // Natural K order: each f32 MFMA substep pairs k = 2t (lanes 0-31)
-          // with k = 2t+1 (lanes 32-63), so every output element is the
-          // k-ordered fmaf chain of the oracle (pmm_oracle.c oracle_gemm_f32)
-          // bit for bit.  Half h reads chunk 2qd+h (k = 8qd+4h..+3) with one
-          // ds_read_b128; two v_permlane32_swap per chunk then trade the
-          // lower half's odd k for the upper half's even k, leaving
-          // regs {0,2,1,3} = k pairs (8qd,+1) (8qd+2,+3) (8qd+4,+5) (8qd+6,+7).
-          const int co = 16 * ((2 * qd + h) ^ swz);
+          // KORDER 0: lane half h covers k = 16h..16h+15 (substep j of group
+          // qd pairs k = 4qd+j with 16+4qd+j).  Otherwise half h reads chunk
+          // 2qd+h: from a gathered image element j is k = 8qd+h+2j, so
+          // substep t = 4qd+j pairs k = 2t (h = 0) with 2t+1 (h = 1) -- every
+          // output is the k-ordered fmaf chain of the oracle bit for bit; from
+          // a plain image (k = 8qd+4h..+3) two v_permlane32_swap trade the
+          // lower half's odd k for the upper half's even k, leaving registers
+          // {0,2,1,3} = k pairs (8qd,+1) (8qd+2,+3) (8qd+4,+5) (8qd+6,+7).
+          const int co = PMM_F32_KORDER == 0 ? 16 * ((4 * h + qd) ^ swz) : 16 * ((2 * qd + h) ^ swz);
           f32x4 av = *(const f32x4 *)(st + a_rd + co);
           f32x4 b[NB];
 #pragma unroll
           for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
+          constexpr bool A_SWAP = PMM_F32_KORDER == 1 || PMM_F32_KORDER == 3;
+          constexpr bool B_SWAP = PMM_F32_KORDER == 1;
           auto kpair = [](f32x4 &x) __attribute__((always_inline)) {
             auto r0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[0]), __float_as_uint(x[1]), false, false);
             auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[2]), __float_as_uint(x[3]), false, false);
@@ -320,17 +309,17 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             x[2] = __uint_as_float(r1[0]);
             x[3] = __uint_as_float(r1[1]);
           };
-          kpair(av);
+          if (A_SWAP) kpair(av);
 #pragma unroll
-          for (int c = 0; c < NB; c++) kpair(b[c]);
-#endif
+          for (int c = 0; c < NB; c++)
+            if (B_SWAP) kpair(b[c]);
 #pragma unroll
           for (int jj = 0; jj < 4; jj++) {
-            // KORDER 1 reads the swapped registers in the order {0, 2, 1, 3}
-            const int j = PMM_F32_KORDER == 1 ? ((jj & 1) << 1) | (jj >> 1) : jj;
+            const int js = ((jj & 1) << 1) | (jj >> 1);  // swapped registers: {0, 2, 1, 3}
+            const int ja = A_SWAP ? js : jj, jb = B_SWAP ? js : jj;
 #pragma unroll
             for (int c = 0; c < NB; c++)
-              acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[j], b[c][j], acc[c], 0, 0, 0);
+              acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ja], b[c][jb], acc[c], 0, 0, 0);
           }
           if (qd < NPART) {
             // next step's LDS-DMA goes out behind the MFMA groups, so the
@@ -619,13 +608,6 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   for (int i = cnt + lane; i < P2; i += 64) scr[i] = 0ull;
   wave_sync();
   wave_sort_desc_u64(scr, P2, lane);
-  if (a.seed_gthr) {
-    if (lane == 0 && cnt >= a.k_out) {
-      const u64 x = scr[a.k_out - 1];
-      if (x != 0ull && x - 1 > a.seed_gthr[row]) a.seed_gthr[row] = x - 1;
-    }
-    return;
-  }
   for (int j = lane; j < a.k_out; j += 64) {
     const u64 x = (j < cnt) ? scr[j] : 0ull;
     uint32_t id = 0xFFFFFFFFu;
@@ -643,6 +625,45 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
 }
 
 size_t merge_lds_bytes_per_wave(int P) { return (size_t)P * 8; }
+
+// ===========================================================================
+// Threshold seeding (topk_f32_device_impl): one wave per query row reads the
+// row's ns exact scores of the corpus sample (materialised by the store-mode
+// GEMM), forms the composite keys (okey(score) << 32 | ~column, the fused
+// kernel's keys) and selects the k-th largest by ballots (wave_kth_u64);
+// gthr[row] = that key - 1, an exact lower bound of the row's final k-th.
+// ===========================================================================
+template <int E>
+__global__ __launch_bounds__(256) void seed_select_kernel(const float *__restrict__ S, int64_t lds, int m,
+                                                          int ns, int k, int metric, u64 *__restrict__ gthr) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= m) return;
+  const float *src = S + (int64_t)row * lds;
+  u64 x[E];
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    const int j = lane + 64 * e;
+    x[e] = 0ull;
+    if (j < ns) {
+      const float v = src[j];
+      x[e] = ((u64)okey32(metric == kMetricEuclidean ? -v : v) << 32) | (u64)(~(uint32_t)j);
+    }
+  }
+  const u64 t = wave_kth_u64<E>(x, k);
+  if (lane == 0 && t != 0ull) gthr[row] = t - 1;
+}
+
+hipError_t launch_seed_select(const float *S, int64_t lds, int m, int ns, int k, int metric,
+                              unsigned long long *gthr, hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  if (ns > kSeedMaxNs || k > ns) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)((m + 3) / 4);
+  if (ns <= 256) seed_select_kernel<4><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
+  else if (ns <= 512) seed_select_kernel<8><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
+  else seed_select_kernel<16><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
+  return hipGetLastError();
+}
 
 hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;

@@ -178,20 +178,32 @@ def test_c5_shape_sharded_1m_bitexact():
     q = _gen(m, d, QSEED, dev)
     c = _gen(n, d, CSEED, dev)
     full_i, full_s = _run_topk(q, c, k)
+    from polars_matmul.sharded import _device_merge
+
+    # the per-rank lists as the RCCL gather lands them on rank 0 (sharded.py):
+    # [world][2][m][k] = per rank an index plane and a score plane
+    gathered = torch.empty((world, 2, m, k), dtype=torch.int32, device=dev)
     lists_i = torch.empty((m, world, k), dtype=torch.int32, device=dev)
     lists_s = torch.empty((m, world, k), dtype=torch.float32, device=dev)
     for r in range(world):
         a, b = shard_bounds(n, world, r)
         li, ls = _run_topk(q, c[a:b], k, index_base=a)
+        gathered[r, 0] = torch.from_numpy(li.view(np.int32)).to(dev)
+        gathered[r, 1] = torch.from_numpy(ls.view(np.int32)).to(dev)
         lists_i[:, r] = torch.from_numpy(li.view(np.int32)).to(dev)
         lists_s[:, r] = torch.from_numpy(ls).to(dev)
     mi = torch.empty((m, k), dtype=torch.int32, device=dev)
     ms = torch.empty((m, k), dtype=torch.float32, device=dev)
-    _native.merge_device(lists_i.data_ptr(), lists_s.data_ptr(), m, world, k, k, COS, mi.data_ptr(),
-                         ms.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    _device_merge(gathered, k, COS, mi, ms)  # the N > 1 rank-0 merge, in place
     torch.cuda.synchronize()
     got_i, got_s = mi.cpu().numpy().view(np.uint32), ms.cpu().numpy()
     assert np.array_equal(got_i, full_i) and np.array_equal(got_s, full_s)
+    # the [m][lists][k] entry point gives the same
+    mi.zero_()
+    _native.merge_device(lists_i.data_ptr(), lists_s.data_ptr(), m, world, k, k, COS, mi.data_ptr(),
+                         ms.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(mi.cpu().numpy().view(np.uint32), full_i)
     qh, ch = q.cpu().numpy(), c.cpu().numpy()
     rows = np.linspace(0, m - 1, 24).astype(np.int64)
     oi, osc = oracle.topk(qh[rows], ch, k, oracle.COSINE, nthreads=THREADS)

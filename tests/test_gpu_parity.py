@@ -734,3 +734,27 @@ def test_threshold_seeding_changes_nothing(pmm, k, monkeypatch):
         assert np.array_equal(got[1], want[1]), metric
         check_topk(got[0], got[1], truth_scores(q, c, metric), metric != "euclidean",
                    label=f"seeded k={k} {metric}")
+
+
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_host_chunked_upload_equals_one_launch(pmm, metric, monkeypatch):
+    # pmm_topk_f32 over a corpus >= 256 MB uploads it in chunks overlapped with
+    # compute (per-chunk top-k with carried thresholds + in-place chunk merge);
+    # the result must equal the one-upload, one-launch result bit for bit,
+    # exact cross-chunk ties included (lower global index first)
+    rs = np.random.RandomState(3 + METRICS[metric])
+    m, n, d = 300, 90_000, 768
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    c[80_000:80_050] = c[10:60]      # chunk 3 duplicates rows of chunk 0
+    c[40_000:40_020] = c[30_000:30_020]  # chunk 2 duplicates rows of chunk 1
+    for k in (1, 100, 1000):
+        monkeypatch.setenv("PMM_CHUNKED_UPLOAD", "0")
+        want = gpu_topk(q, c, k, metric)
+        monkeypatch.delenv("PMM_CHUNKED_UPLOAD")
+        got = gpu_topk(q, c, k, metric)
+        assert np.array_equal(got[0], want[0]), (metric, k)
+        assert np.array_equal(got[1].view(np.uint32), want[1].view(np.uint32)), (metric, k)
+    oi, osc = oracle.topk(q[:40], c, 100, METRICS[metric])
+    got = gpu_topk(q[:40], c, 100, metric)
+    assert_bitexact(got[0], got[1], oi, osc, f"chunked {metric}")
