@@ -274,6 +274,17 @@ bool bf16_ws_enabled(int capg, int64_t d) {
   return capg <= kBf16WsMaxCapg && gemm_bf16_ws_lds_bytes(capg, dp) <= 160 * 1024;
 }
 
+// 256-query-row bf16 kernel (pmm_bf16_wide_kernel.h): opt-in (PMM_BF16_WIDE=1)
+// where its compaction holds the candidate buffer in registers (capg <= 384,
+// k <= 192).  Correct and bit-identical to the wave-specialised kernel, but
+// measured slower at c4, so not the default.  Read per call.
+bool bf16_wide_enabled(int capg, int64_t d) {
+  const char *e = getenv("PMM_BF16_WIDE");
+  if (!e || atoi(e) == 0) return false;
+  const int dp = (int)(cdiv(d, kBf16DAlign) * kBf16DAlign);
+  return capg <= kBf16WideMaxCapg && dp <= kBf16MaxD && gemm_bf16_wide_lds_bytes(dp) <= 160 * 1024;
+}
+
 // compute = PMM_COMPUTE_F32: the f32 kernel (variant chosen by LDS fit);
 // PMM_COMPUTE_BF16: the wave-specialised bf16 kernel (variant -2, 128 x 64
 // tiles, 8 waves) or the 4-wave one (variant -1, 128 x 128 tiles).
@@ -299,10 +310,11 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
     if (cap_env > 0 && k + 64 <= 512) p.capg = std::max<int>(((int)k + 64 + 7) / 8 * 8, std::min(cap_env, 512) / 8 * 8);
   }
   const bool bf16 = compute == PMM_COMPUTE_BF16;
-  const bool ws = bf16 && bf16_ws_enabled(p.capg, d);
-  p.variant = bf16 ? (ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
-  const int bm = bf16 ? kBf16BM : gemm_f32_bm(p.variant);
-  const int bn = bf16 ? (ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
+  const bool wide = bf16 && bf16_wide_enabled(p.capg, d);
+  const bool ws = bf16 && !wide && bf16_ws_enabled(p.capg, d);
+  p.variant = bf16 ? (wide ? -3 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
+  const int bm = bf16 ? (wide ? kBf16WideBM : kBf16BM) : gemm_f32_bm(p.variant);
+  const int bn = bf16 ? (wide ? kBf16WideBN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
   const size_t cand_budget = size_t(8) << 30;
   int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
@@ -319,8 +331,10 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   // f32 kernel: the same split of units (PMM_F32_WHOLE=0: split units only).
   // At c3 the GEMM time is unchanged (1076 ms either way) and the merge reads
   // 0.89 GB instead of 2.17 GB (0.40 vs 0.65 ms).
-  const bool whole = bf16 ? (ws && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
-  plan_units(m, n, bm, bn, cus, bf16 ? (ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
+  const bool whole = bf16 ? ((ws || wide) && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
+  // unit overhead in tiles: a wide unit's query-row load (256 rows x D) is
+  // about ten of its 32-column tiles
+  plan_units(m, n, bm, bn, cus, bf16 ? (wide ? 10.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
   p.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
   size_t off = 0;
   p.off_counter = off;
@@ -710,7 +724,9 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     }
     {
       Timed t("gemm_bf16_topk", s);
-      HIP_TRY(p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s) : launch_gemm_bf16(a, p.grid, s));
+      HIP_TRY(p.variant == -3   ? launch_gemm_bf16_wide(a, p.grid, s)
+              : p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s)
+                                : launch_gemm_bf16(a, p.grid, s));
     }
     if (stats) {
       unsigned long long h[8];

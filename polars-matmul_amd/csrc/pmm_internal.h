@@ -118,6 +118,17 @@ constexpr int kBf16WsBN = 64;
 constexpr int kBf16WsMaxCapg = 512;
 size_t gemm_bf16_ws_lds_bytes(int capg, int D);  // D = padded dimension
 hipError_t launch_gemm_bf16_ws(const GemmF32Args &a, int grid, hipStream_t s);
+// 256-query-row bf16 kernel (pmm_bf16_wide_kernel.h): 8 waves (2 per SIMD),
+// each 32 query rows x D in registers, 32-column corpus tiles; used when capg
+// <= kBf16WideMaxCapg unless PMM_BF16_WIDE=0.
+constexpr int kBf16WideBM = 256, kBf16WideBN = 32;
+constexpr int kBf16WideMaxCapg = 384;  // k <= 192 (the compaction's registers)
+#ifndef PMM_BF16_WIDE_AHEAD
+#define PMM_BF16_WIDE_AHEAD 6
+#endif
+constexpr int kBf16WideAhead = PMM_BF16_WIDE_AHEAD;  // K-steps of corpus DMA in flight
+size_t gemm_bf16_wide_lds_bytes(int D);  // D = padded dimension
+hipError_t launch_gemm_bf16_wide(const GemmF32Args &a, int grid, hipStream_t s);
 // f32 rows -> bf16 (round to nearest even) with row stride ldd, columns
 // d..ldd-1 zero-filled.
 hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t lds, uint16_t *dst,

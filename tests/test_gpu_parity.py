@@ -580,11 +580,44 @@ def test_bf16_one_wave_per_simd_kernel(pmm, m, n, d, k, metric, monkeypatch):
     # PMM_BF16_WS=0: the 4-wave kernel (pmm_bf16_kernel.h) on shapes the
     # wave-specialised kernel serves by default (it still serves k > 448)
     monkeypatch.setenv("PMM_BF16_WS", "0")
+    monkeypatch.setenv("PMM_BF16_WIDE", "0")
     rs = np.random.RandomState(m + n + d + k)
     q = rs.randn(m, d).astype(np.float32)
     c = rs.randn(n, d).astype(np.float32)
     idx, sc = gpu_topk_bf16(q, c, k, metric)
     _bf16_truth_check(q, c, k, metric, idx, sc, f"bf16 classic {m}x{n}x{d} k={k} {metric}")
+
+
+@pytest.mark.parametrize("m,n,d,k", [(130, 257, 33, 7), (257, 4099, 200, 64), (300, 2000, 768, 100),
+                                     (300, 2000, 768, 448)])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_wide_kernel(pmm, m, n, d, k, metric, monkeypatch):
+    # PMM_BF16_WIDE=1: the opt-in 256-row kernel (pmm_bf16_wide_kernel.h; k >
+    # 192 falls back to the wave-specialised kernel) vs float64 truth
+    monkeypatch.setenv("PMM_BF16_WIDE", "1")
+    rs = np.random.RandomState(m + n + d + k + 1)
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    idx, sc = gpu_topk_bf16(q, c, k, metric)
+    _bf16_truth_check(q, c, k, metric, idx, sc, f"bf16 wide {m}x{n}x{d} k={k} {metric}")
+
+
+@pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (520, 40000, 768, 100), (70, 3000, 640, 192)])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_wide_equals_wave_specialised(pmm, m, n, d, k, metric, monkeypatch):
+    # the 256-row kernel (corpus as the MFMA's A operand) and the 128-row
+    # kernel (queries as A) sum the same bf16 products in the same K order:
+    # identical f32 scores, so identical top-k lists, bit for bit
+    rs = np.random.RandomState(m + n + d + k + 2)
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    c[n // 2:n // 2 + 50] = c[:50]  # exact ties across the corpus
+    monkeypatch.setenv("PMM_BF16_WIDE", "0")
+    wi, ws_ = gpu_topk_bf16(q, c, k, metric)
+    monkeypatch.setenv("PMM_BF16_WIDE", "1")
+    gi, gs = gpu_topk_bf16(q, c, k, metric)
+    assert np.array_equal(gi, wi), f"{metric}: {np.mean(gi == wi)}"
+    assert np.array_equal(gs, ws_)
 
 
 def test_bf16_recall_vs_f32(pmm):
@@ -631,20 +664,23 @@ def test_bf16_device_api_many_splits(pmm):
 
 @pytest.mark.parametrize("whole", ["0", "1"])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-def test_bf16_whole_block_runs(pmm, metric, whole, monkeypatch):
-    # M >= 128 x grid query rows.  PMM_BF16_WHOLE=1: the wave-specialised
-    # kernel runs the first 256 query blocks whole (split by split, row state
-    # carried across splits) and the remaining 2 blocks as split units;
-    # default: every unit a split unit.  Every row vs float64 truth.
+@pytest.mark.parametrize("kernel", ["wide", "ws"])
+def test_bf16_whole_block_runs(pmm, metric, whole, kernel, monkeypatch):
+    # M >= BM x grid query rows (BM = 128 for the default wave-specialised
+    # kernel, 256 for the opt-in wide one).  PMM_BF16_WHOLE=1 (default): the first 256 query
+    # blocks run whole (split by split, row state carried across splits), the
+    # remaining 2-3 blocks as split units; 0: every unit a split unit.  Every
+    # row vs float64 truth.
     import torch
 
     monkeypatch.setenv("PMM_BF16_WHOLE", whole)
+    monkeypatch.setenv("PMM_BF16_WIDE", "1" if kernel == "wide" else "0")
 
     n = _native()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(11)
-    m, N, d, k = 33000, 30000, 256, 50
+    m, N, d, k = (66000 if kernel == "wide" else 33000), 30000, 256, 50
     q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
     c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
     oi = torch.empty((m, k), dtype=torch.int32, device=dev)
