@@ -576,7 +576,13 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
       else HIP_TRY(launch_norms_pair_f32(q, m, ldq, qn, c, n, ldc, cn, cn + n, d, sq, s));
     }
     FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
-    if (seed) {
+    if (seed && dp <= kSeedDotsMaxD && ldq % 4 == 0 && ldc % 4 == 0 && !(((uintptr_t)q | (uintptr_t)c) & 15) &&
+        !getenv("PMM_SEED_GEMM")) {
+      // one launch: the sample's scores as fmaf chains + the per-row select
+      Timed t("gemm_f32_seed", s);
+      HIP_TRY(launch_seed_dots(q, ldq, (int)m, c, ldc, (int)ns, (int)dp, qn, cn, (int)k, metric,
+                               (unsigned long long *)(w + p.off_gthr), s));
+    } else if (seed) {
       float *sample = (float *)(w + p.off_cand);
       int rc = gemm_store_f32(q, ldq, m, c, ldc, ns, dp, metric, 1, qn, cn, sample, ns,
                               (unsigned *)(w + p.off_counter) + 16, cus, s, "gemm_f32_seed", true);

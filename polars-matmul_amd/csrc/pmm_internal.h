@@ -100,6 +100,12 @@ hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s);
 // Threshold seeding: gthr[row] = (k-th best composite of the row's ns
 // materialised scores S[row][0..ns)) - 1, one wave per row; ns <= kSeedMaxNs.
 constexpr int kSeedMaxNs = 1024;
+// The same threshold from one launch that computes the sample's scores itself
+// (fmaf chains, bit-identical to the fused kernel's): padded dp <= kSeedDotsMaxD.
+constexpr int kSeedDotsMaxD = 2048;
+hipError_t launch_seed_dots(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int ns, int dp,
+                            const float *qn, const float *cn, int k, int metric, unsigned long long *gthr,
+                            hipStream_t s);
 hipError_t launch_seed_select(const float *S, int64_t lds, int m, int ns, int k, int metric,
                               unsigned long long *gthr, hipStream_t s);
 // ---- bf16 compute path (pmm_bf16.hip) ----

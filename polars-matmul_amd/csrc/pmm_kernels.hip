@@ -665,6 +665,118 @@ hipError_t launch_seed_select(const float *S, int64_t lds, int m, int ns, int k,
   return hipGetLastError();
 }
 
+// Threshold seeding in one launch: a block takes 4 query rows (staged in
+// LDS) and all ns sample columns, thread t columns t, t + 256, ...; each
+// thread runs its 4 dot products as fmaf chains in natural K order over the
+// padded dimension -- the fused kernel's v_mfma_f32_32x32x2_f32 chain bit
+// for bit -- then exact_score; the keys go to LDS and wave w selects row w's
+// k-th (as above).  Replaces the store-mode GEMM over the sample plus
+// seed_select_kernel and a launch gap at small sizes (c1: 28 us against
+// 32 + 8 us).  Its per-lane row reads thrash the vector L1 (64 rows per load
+// instruction); an LDS-staged variant with coalesced loads measured slower
+// (87 us: its load and compute phases serialise), as did batching each
+// lane's loads 8 deep (39 us).
+namespace seedk {
+constexpr int RQ = 4;  // query rows per block (one per wave for the selection)
+}  // namespace seedk
+template <int E, int METRIC>
+__global__ __launch_bounds__(256) void seed_dots_kernel(const float *__restrict__ q, int64_t ldq, int m,
+                                                        const float *__restrict__ c, int64_t ldc, int ns, int dp,
+                                                        const float *__restrict__ qn, const float *__restrict__ cn,
+                                                        int k, u64 *__restrict__ gthr) {
+  using namespace seedk;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  u64 *keys = (u64 *)smem;                        // [RQ][64 E]
+  float *qs = (float *)(smem + RQ * 64 * E * 8);  // [RQ][dp]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int row0 = blockIdx.x * RQ;
+  for (int r = 0; r < RQ; r++)
+    for (int j4 = tid; j4 < dp / 4; j4 += 256) {
+      f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (row0 + r < m) v = *(const f32x4 *)(q + (int64_t)(row0 + r) * ldq + 4 * j4);
+      *(f32x4 *)(qs + r * dp + 4 * j4) = v;
+    }
+  __syncthreads();
+  for (int col = tid; col < 64 * E; col += 256) {
+    float acc[RQ];
+#pragma unroll
+    for (int r = 0; r < RQ; r++) acc[r] = 0.0f;
+    if (col < ns) {
+      const f32x4 *cr = (const f32x4 *)(c + (int64_t)col * ldc);
+      for (int j4 = 0; j4 < dp / 4; j4++) {
+        const f32x4 cv = cr[j4];
+#pragma unroll
+        for (int r = 0; r < RQ; r++) {
+          const f32x4 q4 = *(const f32x4 *)(qs + r * dp + 4 * j4);  // broadcast
+          acc[r] = fmaf(q4[0], cv[0], acc[r]);
+          acc[r] = fmaf(q4[1], cv[1], acc[r]);
+          acc[r] = fmaf(q4[2], cv[2], acc[r]);
+          acc[r] = fmaf(q4[3], cv[3], acc[r]);
+        }
+      }
+    }
+    const float cv = (METRIC != kMetricDot && col < ns) ? cn[col] : 0.0f;
+#pragma unroll
+    for (int r = 0; r < RQ; r++) {
+      u64 key = 0ull;
+      if (col < ns && row0 + r < m) {
+        const float qv = (METRIC != kMetricDot) ? qn[row0 + r] : 0.0f;
+        const float sc = exact_score<METRIC>(acc[r], qv, cv);
+        key = ((u64)okey32(METRIC == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~(uint32_t)col);
+      }
+      keys[r * 64 * E + col] = key;
+    }
+  }
+  __syncthreads();
+  const int row = row0 + w;
+  if (row >= m) return;
+  u64 x[E];
+#pragma unroll
+  for (int e = 0; e < E; e++) x[e] = keys[w * 64 * E + lane + 64 * e];
+  const u64 th = wave_kth_u64<E>(x, k);
+  if (lane == 0 && th != 0ull) gthr[row] = th - 1;
+}
+
+template <int METRIC>
+static hipError_t launch_seed_dots_t(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int ns,
+                                     int dp, const float *qn, const float *cn, int k, unsigned long long *gthr,
+                                     hipStream_t s) {
+  using namespace seedk;
+  const unsigned grid = (unsigned)((m + RQ - 1) / RQ);
+  const size_t lds_base = (size_t)RQ * dp * 4;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void *)seed_dots_kernel<4, METRIC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)(lds_base + RQ * 256 * 8));
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void *)seed_dots_kernel<8, METRIC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(lds_base + RQ * 512 * 8));
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void *)seed_dots_kernel<16, METRIC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(lds_base + RQ * 1024 * 8));
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  if (ns <= 256) seed_dots_kernel<4, METRIC><<<grid, 256, lds_base + RQ * 256 * 8, s>>>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr);
+  else if (ns <= 512) seed_dots_kernel<8, METRIC><<<grid, 256, lds_base + RQ * 512 * 8, s>>>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr);
+  else seed_dots_kernel<16, METRIC><<<grid, 256, lds_base + RQ * 1024 * 8, s>>>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr);
+  return hipGetLastError();
+}
+
+hipError_t launch_seed_dots(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int ns, int dp,
+                            const float *qn, const float *cn, int k, int metric, unsigned long long *gthr,
+                            hipStream_t s) {
+  if (m <= 0) return hipSuccess;
+  // the kernel's shapes: whole float4 groups of padded rows, a sample its
+  // LDS holds, 16-byte aligned rows
+  if (ns > kSeedMaxNs || k > ns || dp % 4 != 0 || dp > kSeedDotsMaxD || ldq % 4 != 0 || ldc % 4 != 0 ||
+      ((uintptr_t)q & 15) || ((uintptr_t)c & 15))
+    return hipErrorInvalidValue;
+  if (metric == kMetricCosine) return launch_seed_dots_t<kMetricCosine>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr, s);
+  if (metric == kMetricDot) return launch_seed_dots_t<kMetricDot>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr, s);
+  return launch_seed_dots_t<kMetricEuclidean>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr, s);
+}
+
 hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
   int wpb = (int)(65536 / merge_lds_bytes_per_wave(a.P));

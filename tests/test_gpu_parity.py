@@ -748,15 +748,18 @@ def test_bf16_numpy_api_and_sharded_runner(pmm):
     assert np.array_equal(osc.cpu().numpy().astype(np.float64), s1)
 
 
-@pytest.mark.parametrize("k", [1, 10, 100])
-def test_threshold_seeding_changes_nothing(pmm, k, monkeypatch):
-    # small problems run a seed pass over the corpus's first rows and start
-    # the main pass from (its k-th composite key - 1); the result must equal
-    # the unseeded run bit for bit, ties (duplicated corpus rows) included
+@pytest.mark.parametrize("k,d", [(1, 256), (10, 256), (100, 256), (10, 72), (10, 768)])
+def test_threshold_seeding_changes_nothing(pmm, k, d, monkeypatch):
+    # small problems seed each row's threshold from the corpus's first rows
+    # (seed_dots_kernel: the sample's scores as fmaf chains, bit-identical to
+    # the fused kernel's MFMA chain; PMM_SEED_GEMM=1: the store-mode GEMM +
+    # seed_select_kernel) and start the main pass from (the sample's k-th
+    # composite key - 1); the result must equal the unseeded run bit for bit,
+    # ties (duplicated corpus rows) included
     from golden.make_golden import truth_scores
 
-    rs = np.random.RandomState(31 + k)
-    m, N, d = 700, 9000, 256
+    rs = np.random.RandomState(31 + k + d)
+    m, N = 700, 9000
     q = rs.randn(m, d).astype(np.float32)
     c = rs.randn(N, d).astype(np.float32)
     c[4000:4600] = c[:600]  # duplicates of sampled rows, later in the corpus
@@ -765,9 +768,13 @@ def test_threshold_seeding_changes_nothing(pmm, k, monkeypatch):
         want = gpu_topk(q, c, k, metric)
         monkeypatch.setenv("PMM_SEED", "1")
         got = gpu_topk(q, c, k, metric)
+        monkeypatch.setenv("PMM_SEED_GEMM", "1")
+        got_g = gpu_topk(q, c, k, metric)
+        monkeypatch.delenv("PMM_SEED_GEMM")
         monkeypatch.delenv("PMM_SEED")
-        assert np.array_equal(got[0], want[0]), metric
-        assert np.array_equal(got[1], want[1]), metric
+        for g in (got, got_g):
+            assert np.array_equal(g[0], want[0]), metric
+            assert np.array_equal(g[1], want[1]), metric
         check_topk(got[0], got[1], truth_scores(q, c, metric), metric != "euclidean",
                    label=f"seeded k={k} {metric}")
 
