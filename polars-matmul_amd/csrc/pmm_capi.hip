@@ -547,15 +547,16 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     // problems: the reference's own benchmark size), a unit starts cold: its
     // first tile's scores nearly all survive the pre-filter and are re-scored
     // exactly, appended and compacted, which took most of the kernel's time.
-    // Instead, the scores of the first ns corpus rows are computed first by
-    // the same MFMA main loop in store mode (the same natural-K-order chain
-    // and epilogue arithmetic, so bit-identical to the main pass's scores) into
-    // the still unused candidate buffers, and one wave per row selects the
-    // k-th best composite of that sample (seed_select_kernel): (that key - 1)
-    // is an exact lower bound of the row's final k-th best and seeds the
-    // shared threshold.  Two short launches instead of round 1's fused seed
-    // pass + merge (0.09 ms at c1).
-    int64_t ns = std::min<int64_t>(n, next_pow2((int)std::max<int64_t>(512, 8 * k), 256));
+    // Instead, the scores of the first ns corpus rows are computed first --
+    // by seed_dots_kernel as fmaf chains in natural K order (bit-identical to
+    // the main pass's MFMA chain and epilogue arithmetic), or, past its
+    // limits or with PMM_SEED_GEMM=1, by the MFMA main loop in store mode into
+    // the still unused candidate buffers -- and one wave per row selects the
+    // k-th best composite of that sample: (that key - 1) is an exact lower
+    // bound of the row's final k-th best and seeds the shared threshold.
+    // Sample size max(256, 8k): at c1 128 / 256 / 512 / 1024 rows measured
+    // 0.170 / 0.163 / 0.174 / 0.192 ms per call (tools/gpu_seedns.sh).
+    int64_t ns = std::min<int64_t>(n, next_pow2((int)std::max<int64_t>(256, 8 * k), 256));
     if (const char *ne = getenv("PMM_SEED_NS")) ns = std::min<int64_t>(n, std::max<int64_t>(atoll(ne), k));
     const char *se = getenv("PMM_SEED");
     bool seed = (se ? atoi(se) != 0 : ((int64_t)p.tps * gemm_f32_bn(p.variant) < 8192 && n >= 4 * ns)) &&
@@ -563,17 +564,21 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
                 (size_t)m * ns * 4 <= p.off_qn - p.off_cand;
     // one fill zeroes the work counters (the main pass's and the seed store
     // pass's), thresholds and buffer counts [0, off_cand)
+    // (with the norms pair kernel the fill rides in the same launch)
+    const bool fill_in_norms =
+        metric != kMetricDot && !c_norms && !keep_gthr && p.off_cand % 16 == 0 && ((uintptr_t)w & 15) == 0;
     if (keep_gthr) {
       HIP_TRY(hipMemsetAsync(w + p.off_counter, 0, p.off_gthr - p.off_counter, s));
       HIP_TRY(hipMemsetAsync(w + p.off_cnt, 0, p.off_cand - p.off_cnt, s));
-    } else {
+    } else if (!fill_in_norms) {
       HIP_TRY(hipMemsetAsync(w, 0, p.off_cand, s));
     }
     if (metric != kMetricDot) {
       const int sq = metric == kMetricEuclidean;
       Timed t("norms_f32", s);
       if (c_norms) HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
-      else HIP_TRY(launch_norms_pair_f32(q, m, ldq, qn, c, n, ldc, cn, cn + n, d, sq, s));
+      else HIP_TRY(launch_norms_pair_f32(q, m, ldq, qn, c, n, ldc, cn, cn + n, d, sq, s,
+                                         fill_in_norms ? w : nullptr, fill_in_norms ? p.off_cand : 0));
     }
     FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
     if (seed && dp <= kSeedDotsMaxD && ldq % 4 == 0 && ldc % 4 == 0 && !(((uintptr_t)q | (uintptr_t)c) & 15) &&

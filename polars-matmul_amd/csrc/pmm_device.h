@@ -254,18 +254,26 @@ __global__ __launch_bounds__(256) void norms_kernel(const TI *__restrict__ a, in
 }
 
 // Query and corpus norms in one launch: blocks [0, qblocks) take the query
-// rows, the rest the corpus rows (same arithmetic as two norms_kernel launches).
+// rows, blocks [qblocks, nblocks) the corpus rows (same arithmetic as two
+// norms_kernel launches), and any blocks past nblocks zero `zn` 16-byte words
+// at `zero` (the fused top-k's counters, so no separate fill launch).
 template <typename T>
 __global__ __launch_bounds__(256) void norms_pair_kernel(const T *__restrict__ q, int64_t m, int64_t ldq,
                                                          T *__restrict__ qout, const T *__restrict__ c,
                                                          int64_t n, int64_t ldc, T *__restrict__ cout,
                                                          T *__restrict__ cinv, int64_t d, int squared,
-                                                         unsigned qblocks) {
-  if (blockIdx.x < qblocks)
+                                                         unsigned qblocks, unsigned nblocks,
+                                                         uint4 *__restrict__ zero, int64_t zn) {
+  if (blockIdx.x < qblocks) {
     norms_rows<T, T>(q, m, d, ldq, squared, qout, nullptr, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
-  else
+  } else if (blockIdx.x < nblocks) {
     norms_rows<T, T>(c, n, d, ldc, squared, cout, cinv,
                      (int64_t)(blockIdx.x - qblocks) * blockDim.x + threadIdx.x);
+  } else {
+    const int64_t stride = (int64_t)(gridDim.x - nblocks) * blockDim.x;
+    for (int64_t i = (int64_t)(blockIdx.x - nblocks) * blockDim.x + threadIdx.x; i < zn; i += stride)
+      zero[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
 }
 
 // ===========================================================================

@@ -82,9 +82,10 @@ struct RowSelArgs {
 };
 
 // ---- launchers (pmm_kernels.hip) ----
+// (also zeroes zero_bytes at zero, a multiple of 16 at a 16-byte address)
 hipError_t launch_norms_pair_f32(const float *q, int64_t m, int64_t ldq, float *qout, const float *c,
                                  int64_t n, int64_t ldc, float *cout, float *cinv, int64_t d, int squared,
-                                 hipStream_t s);
+                                 hipStream_t s, void *zero = nullptr, size_t zero_bytes = 0);
 hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld, int squared,
                             float *out, float *inv, hipStream_t s);
 hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,

@@ -16,6 +16,8 @@
 // the epilogue arithmetic follows the reference's operation order.
 #include "pmm_device.h"
 
+#include <algorithm>
+
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
@@ -32,10 +34,14 @@ hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld,
 }
 hipError_t launch_norms_pair_f32(const float *q, int64_t m, int64_t ldq, float *qout, const float *c,
                                  int64_t n, int64_t ldc, float *cout, float *cinv, int64_t d, int squared,
-                                 hipStream_t s) {
+                                 hipStream_t s, void *zero, size_t zero_bytes) {
   const unsigned gq = (unsigned)((m * 8 + 255) / 256), gc = (unsigned)((n * 8 + 255) / 256);
-  if (gq + gc == 0) return hipSuccess;
-  norms_pair_kernel<float><<<gq + gc, 256, 0, s>>>(q, m, ldq, qout, c, n, ldc, cout, cinv, d, squared, gq);
+  if (zero_bytes % 16 != 0 || ((uintptr_t)zero & 15)) return hipErrorInvalidValue;
+  const int64_t zn = (int64_t)(zero_bytes / 16);
+  const unsigned gz = (unsigned)std::min<int64_t>((zn + 255) / 256, 64);
+  if (gq + gc + gz == 0) return hipSuccess;
+  norms_pair_kernel<float><<<gq + gc + gz, 256, 0, s>>>(q, m, ldq, qout, c, n, ldc, cout, cinv, d, squared, gq,
+                                                        gq + gc, (uint4 *)zero, zn);
   return hipGetLastError();
 }
 hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,
