@@ -555,7 +555,7 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     // k-th best composite of that sample: (that key - 1) is an exact lower
     // bound of the row's final k-th best and seeds the shared threshold.
     // Sample size max(256, 8k): at c1 128 / 256 / 512 / 1024 rows measured
-    // 0.170 / 0.163 / 0.174 / 0.192 ms per call (tools/gpu_seedns.sh).
+    // 0.170 / 0.163 / 0.174 / 0.192 ms per call (tools/experiments/gpu_seedns.sh).
     int64_t ns = std::min<int64_t>(n, next_pow2((int)std::max<int64_t>(256, 8 * k), 256));
     if (const char *ne = getenv("PMM_SEED_NS")) ns = std::min<int64_t>(n, std::max<int64_t>(atoll(ne), k));
     const char *se = getenv("PMM_SEED");
