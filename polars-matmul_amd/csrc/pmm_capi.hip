@@ -335,7 +335,10 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   // unit overhead in tiles: a wide unit's query-row load (256 rows x D) is
   // about ten of its 32-column tiles
   plan_units(m, n, bm, bn, cus, bf16 ? (wide ? 10.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
-  p.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
+  // merge_kernel's per-row LDS capacity: at least 512, so a row's candidate
+  // lists rarely need a compaction before the final one (c1: ~400 survivors
+  // of the seed threshold per row; P = 128 compacted ~6 times, 23 us)
+  p.P = std::min(8192, std::max(512, next_pow2(2 * (int)k + 64, 128)));
   size_t off = 0;
   p.off_counter = off;
   off += 256;
@@ -562,39 +565,47 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     bool seed = (se ? atoi(se) != 0 : ((int64_t)p.tps * gemm_f32_bn(p.variant) < 8192 && n >= 4 * ns)) &&
                 ns >= k && ns < n && ns <= kSeedMaxNs && !keep_gthr &&
                 (size_t)m * ns * 4 <= p.off_qn - p.off_cand;
-    // one fill zeroes the work counters (the main pass's and the seed store
-    // pass's), thresholds and buffer counts [0, off_cand)
-    // (with the norms pair kernel the fill rides in the same launch)
-    const bool fill_in_norms =
-        metric != kMetricDot && !c_norms && !keep_gthr && p.off_cand % 16 == 0 && ((uintptr_t)w & 15) == 0;
-    if (keep_gthr) {
-      HIP_TRY(hipMemsetAsync(w + p.off_counter, 0, p.off_gthr - p.off_counter, s));
-      HIP_TRY(hipMemsetAsync(w + p.off_cnt, 0, p.off_cand - p.off_cnt, s));
-    } else if (!fill_in_norms) {
-      HIP_TRY(hipMemsetAsync(w, 0, p.off_cand, s));
-    }
-    if (metric != kMetricDot) {
-      const int sq = metric == kMetricEuclidean;
-      Timed t("norms_f32", s);
-      if (c_norms) HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
-      else HIP_TRY(launch_norms_pair_f32(q, m, ldq, qn, c, n, ldc, cn, cn + n, d, sq, s,
-                                         fill_in_norms ? w : nullptr, fill_in_norms ? p.off_cand : 0));
-    }
     FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
-    if (seed && dp <= kSeedDotsMaxD && ldq % 4 == 0 && ldc % 4 == 0 && !(((uintptr_t)q | (uintptr_t)c) & 15) &&
-        !getenv("PMM_SEED_GEMM")) {
-      // one launch: the sample's scores as fmaf chains + the per-row select
+    // Seeded small problems: one prologue launch (seed + norms + fills).
+    const bool one_prologue = seed && dp <= kSeedDotsMaxD && ldq % 4 == 0 && ldc % 4 == 0 &&
+                              !(((uintptr_t)q | (uintptr_t)c | (uintptr_t)w) & 15) && p.off_gthr % 16 == 0 &&
+                              p.off_cnt % 16 == 0 && p.off_cand % 16 == 0 && !getenv("PMM_SEED_GEMM");
+    if (one_prologue) {
       Timed t("gemm_f32_seed", s);
-      HIP_TRY(launch_seed_dots(q, ldq, (int)m, c, ldc, (int)ns, (int)dp, qn, cn, (int)k, metric,
-                               (unsigned long long *)(w + p.off_gthr), s));
-    } else if (seed) {
-      float *sample = (float *)(w + p.off_cand);
-      int rc = gemm_store_f32(q, ldq, m, c, ldc, ns, dp, metric, 1, qn, cn, sample, ns,
-                              (unsigned *)(w + p.off_counter) + 16, cus, s, "gemm_f32_seed", true);
-      if (rc) return rc;
-      Timed t("seed_select", s);
-      HIP_TRY(launch_seed_select(sample, ns, (int)m, (int)ns, (int)k, metric,
-                                 (unsigned long long *)(w + p.off_gthr), s));
+      HIP_TRY(launch_seeded_prologue(q, ldq, (int)m, c, ldc, n, (int)d, (int)dp, (int)ns, (int)k, metric, qn, cn,
+                                     !c_norms, (unsigned long long *)(w + p.off_gthr), w, p.off_gthr,
+                                     w + p.off_cnt, p.off_cand - p.off_cnt, s));
+    } else {
+      // one fill zeroes the work counters (the main pass's and the seed store
+      // pass's), thresholds and buffer counts [0, off_cand); with the norms
+      // pair kernel the fill rides in the same launch
+      const bool fill_in_norms =
+          metric != kMetricDot && !c_norms && !keep_gthr && p.off_cand % 16 == 0 && ((uintptr_t)w & 15) == 0;
+      if (keep_gthr) {
+        HIP_TRY(hipMemsetAsync(w + p.off_counter, 0, p.off_gthr - p.off_counter, s));
+        HIP_TRY(hipMemsetAsync(w + p.off_cnt, 0, p.off_cand - p.off_cnt, s));
+      } else if (!fill_in_norms) {
+        HIP_TRY(hipMemsetAsync(w, 0, p.off_cand, s));
+      }
+      if (metric != kMetricDot) {
+        const int sq = metric == kMetricEuclidean;
+        Timed t("norms_f32", s);
+        if (c_norms) HIP_TRY(launch_norms_f32(q, m, d, ldq, sq, qn, nullptr, s));
+        else HIP_TRY(launch_norms_pair_f32(q, m, ldq, qn, c, n, ldc, cn, cn + n, d, sq, s,
+                                           fill_in_norms ? w : nullptr, fill_in_norms ? p.off_cand : 0));
+      }
+      if (seed) {
+        // PMM_SEED_GEMM=1 or outside the one-launch limits: the sample's
+        // scores from the fused kernel's main loop in store mode, then a
+        // select launch
+        float *sample = (float *)(w + p.off_cand);
+        int rc = gemm_store_f32(q, ldq, m, c, ldc, ns, dp, metric, 1, qn, cn, sample, ns,
+                                (unsigned *)(w + p.off_counter) + 16, cus, s, "gemm_f32_seed", true);
+        if (rc) return rc;
+        Timed t("seed_select", s);
+        HIP_TRY(launch_seed_select(sample, ns, (int)m, (int)ns, (int)k, metric,
+                                   (unsigned long long *)(w + p.off_gthr), s));
+      }
     }
     HIP_TRY(run_fused_f32(f, p, w, index_base, out_idx, out_score, "gemm_f32_topk", "merge_topk", s));
     return own ? arena_record(dev, s) : PMM_OK;

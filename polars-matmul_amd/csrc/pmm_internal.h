@@ -101,12 +101,16 @@ hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s);
 // Threshold seeding: gthr[row] = (k-th best composite of the row's ns
 // materialised scores S[row][0..ns)) - 1, one wave per row; ns <= kSeedMaxNs.
 constexpr int kSeedMaxNs = 1024;
-// The same threshold from one launch that computes the sample's scores itself
-// (fmaf chains, bit-identical to the fused kernel's): padded dp <= kSeedDotsMaxD.
+// The fused top-k's prologue with threshold seeding in one launch: the seed
+// (the sample's scores as fmaf chains, bit-identical to the fused kernel's,
+// with its own norms; writes every row's gthr), the query norms (and the
+// corpus norms when corpus_norms), and zeroing [z0, +z0_bytes) and [z1,
+// +z1_bytes).  Padded dp <= kSeedDotsMaxD.
 constexpr int kSeedDotsMaxD = 2048;
-hipError_t launch_seed_dots(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int ns, int dp,
-                            const float *qn, const float *cn, int k, int metric, unsigned long long *gthr,
-                            hipStream_t s);
+hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int64_t n,
+                                  int d, int dp, int ns, int k, int metric, float *qn, float *cn, bool corpus_norms,
+                                  unsigned long long *gthr, void *z0, size_t z0_bytes, void *z1, size_t z1_bytes,
+                                  hipStream_t s);
 hipError_t launch_seed_select(const float *S, int64_t lds, int m, int ns, int k, int metric,
                               unsigned long long *gthr, hipStream_t s);
 // ---- bf16 compute path (pmm_bf16.hip) ----

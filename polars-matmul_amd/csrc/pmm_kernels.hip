@@ -567,11 +567,49 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
       cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
     }
   };
-  if (a.S <= 64) {
-    // All list lengths in one load (lane s holds list s's), then the lists'
-    // 64-entry chunks as one flat sequence, MU chunk loads in flight at a
-    // time: the row's reads no longer wait on one another (HBM latency, not
-    // bandwidth, bounded the per-list loop).
+  if (LOADER == 0 && a.S <= 64) {
+    // All list lengths in one load (lane s holds list s's), their prefix sum
+    // across the wave, then the row's candidates as ONE flat sequence: slot j
+    // finds its list by a binary search over the prefix sums (lane shuffles)
+    // and MU x 64 slots are loaded at a time.  Short lists (small problems:
+    // a few entries in each of ~30 lists) then cost one round of loads, not
+    // one per list.
+    constexpr int MU = 4;
+    const int nl = (lane < a.S) ? (int)a.cnt[(int64_t)row * a.S + lane] : 0;
+    int incl = nl;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += t;
+    }
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    for (int base = 0; base < total; base += 64 * MU) {
+      u64 x[MU];
+#pragma unroll
+      for (int u = 0; u < MU; u++) {
+        const int j = base + 64 * u + lane;
+        // list s: the first with incl_s > j (incl is non-decreasing)
+        int lo = 0, hi = a.S - 1;
+#pragma unroll
+        for (int it = 0; it < 6; it++) {
+          const int mid = (lo + hi) >> 1;
+          const int v = __shfl(incl, mid, 64);
+          if (lo < hi) {
+            if (v > j) hi = mid;
+            else lo = mid + 1;
+          }
+        }
+        const int sj = lo;
+        const int excl = __shfl(incl, sj, 64) - __shfl(nl, sj, 64);
+        x[u] = (j < total) ? a.cand[((int64_t)row * a.S + sj) * a.capg + (j - excl)] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < MU; u++) take(x[u]);
+    }
+  } else if (a.S <= 64) {
+    // (gathered per-rank lists: all the same length) all list lengths in one
+    // load (lane s holds list s's), then the lists' 64-entry chunks as one
+    // flat sequence, MU chunk loads in flight at a time
     constexpr int MU = 4;
     const int nl = (lane < a.S) ? ((LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + lane] : a.k_in) : 0;
     int s = 0, c = 0;
@@ -671,44 +709,93 @@ hipError_t launch_seed_select(const float *S, int64_t lds, int m, int ns, int k,
   return hipGetLastError();
 }
 
-// Threshold seeding in one launch: a block takes 4 query rows (staged in
-// LDS) and all ns sample columns, thread t columns t, t + 256, ...; each
-// thread runs its 4 dot products as fmaf chains in natural K order over the
-// padded dimension -- the fused kernel's v_mfma_f32_32x32x2_f32 chain bit
-// for bit -- then exact_score; the keys go to LDS and wave w selects row w's
-// k-th (as above).  Replaces the store-mode GEMM over the sample plus
-// seed_select_kernel and a launch gap at small sizes (c1: 28 us against
-// 32 + 8 us).  Its per-lane row reads thrash the vector L1 (64 rows per load
-// instruction); an LDS-staged variant with coalesced loads measured slower
-// (87 us: its load and compute phases serialise), as did batching each
-// lane's loads 8 deep (39 us).
+// The fused top-k's prologue in one launch (small problems, with threshold
+// seeding): seed blocks first, then the query and corpus norms blocks, then
+// blocks zeroing the work counters and candidate counts.
+//
+// A seed block takes 4 query rows (staged in LDS) and all ns sample columns,
+// thread t columns t, t + 256, ...; each thread runs its 4 dot products as
+// fmaf chains in natural K order over the padded dimension -- the fused
+// kernel's v_mfma_f32_32x32x2_f32 chain bit for bit -- and, for the
+// normalising metrics, its column's norm in ndarray's unrolled order from the
+// same loaded values (norms_rows' arithmetic bit for bit); the 4 row norms
+// come from norms_rows over the staged rows.  exact_score gives the scores;
+// their composite keys go to LDS and wave w writes row w's threshold
+// (k-th key - 1).  So the seed needs nothing from the norms blocks and shares
+// their launch.  (Round 1: a store-mode pass of the fused kernel + a select
+// launch, 32 + 8 us at c1, on 32 workgroups.)  Its per-lane row reads thrash
+// the vector L1 (64 rows per load instruction); an LDS-staged variant with
+// coalesced loads measured slower (87 us: its load and compute phases
+// serialise), as did batching each lane's loads 8 deep (39 us against 28).
 namespace seedk {
-constexpr int RQ = 4;  // query rows per block (one per wave for the selection)
+constexpr int RQ = 4;  // query rows per seed block (one per wave for the selection)
 }  // namespace seedk
+struct PrologueArgs {
+  const float *q;
+  int64_t ldq;
+  int m;
+  const float *c;
+  int64_t ldc;
+  int64_t n;
+  int d, dp, ns, k, squared;
+  float *qn, *cn, *cinv;       // norms outputs (cn / cinv unused when cblocks = 0)
+  unsigned long long *gthr;    // seed outputs: every row's threshold
+  uint4 *z0, *z1;              // zeroed ranges (16-byte words)
+  int64_t z0n, z1n;
+  unsigned sblocks, qblocks, cblocks, zblocks;
+};
 template <int E, int METRIC>
-__global__ __launch_bounds__(256) void seed_dots_kernel(const float *__restrict__ q, int64_t ldq, int m,
-                                                        const float *__restrict__ c, int64_t ldc, int ns, int dp,
-                                                        const float *__restrict__ qn, const float *__restrict__ cn,
-                                                        int k, u64 *__restrict__ gthr) {
+__global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   using namespace seedk;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  unsigned b = blockIdx.x;
+  if (b >= a.sblocks) {
+    b -= a.sblocks;
+    if (b < a.qblocks) {
+      norms_rows<float, float>(a.q, a.m, a.d, a.ldq, a.squared, a.qn, nullptr, (int64_t)b * 256 + tid);
+      return;
+    }
+    b -= a.qblocks;
+    if (b < a.cblocks) {
+      norms_rows<float, float>(a.c, a.n, a.d, a.ldc, a.squared, a.cn, a.cinv, (int64_t)b * 256 + tid);
+      return;
+    }
+    b -= a.cblocks;
+    const int64_t stride = (int64_t)a.zblocks * 256;
+    for (int64_t i = (int64_t)b * 256 + tid; i < a.z0n + a.z1n; i += stride) {
+      if (i < a.z0n) a.z0[i] = make_uint4(0u, 0u, 0u, 0u);
+      else a.z1[i - a.z0n] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    return;
+  }
+  constexpr bool XFORM = METRIC != kMetricDot;
+  const int dp = a.dp, d = a.d, ns = a.ns, m = a.m;
   u64 *keys = (u64 *)smem;                        // [RQ][64 E]
   float *qs = (float *)(smem + RQ * 64 * E * 8);  // [RQ][dp]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int row0 = blockIdx.x * RQ;
+  float *qn_s = qs + RQ * dp;                     // [RQ]
+  const int row0 = b * RQ;
   for (int r = 0; r < RQ; r++)
     for (int j4 = tid; j4 < dp / 4; j4 += 256) {
       f32x4 v = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (row0 + r < m) v = *(const f32x4 *)(q + (int64_t)(row0 + r) * ldq + 4 * j4);
+      if (row0 + r < m) v = *(const f32x4 *)(a.q + (int64_t)(row0 + r) * a.ldq + 4 * j4);
       *(f32x4 *)(qs + r * dp + 4 * j4) = v;
     }
   __syncthreads();
+  if (XFORM && w == 0) norms_rows<float, float>(qs, RQ, d, dp, a.squared, qn_s, nullptr, tid);
+  __syncthreads();
+  const int d8 = d & ~7;
   for (int col = tid; col < 64 * E; col += 256) {
     float acc[RQ];
 #pragma unroll
     for (int r = 0; r < RQ; r++) acc[r] = 0.0f;
+    float p[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) p[j] = 0.0f;
+    float cnv = 0.0f;
     if (col < ns) {
-      const f32x4 *cr = (const f32x4 *)(c + (int64_t)col * ldc);
+      const float *crow = a.c + (int64_t)col * a.ldc;
+      const f32x4 *cr = (const f32x4 *)crow;
       for (int j4 = 0; j4 < dp / 4; j4++) {
         const f32x4 cv = cr[j4];
 #pragma unroll
@@ -719,15 +806,31 @@ __global__ __launch_bounds__(256) void seed_dots_kernel(const float *__restrict_
           acc[r] = fmaf(q4[2], cv[2], acc[r]);
           acc[r] = fmaf(q4[3], cv[3], acc[r]);
         }
+        if (XFORM && 4 * j4 < d8) {
+          // ndarray order: accumulator j sums x[8t + j]^2 over t
+          const int o = (j4 & 1) * 4;
+#pragma unroll
+          for (int e = 0; e < 4; e++) p[o + e] = p[o + e] + cv[e] * cv[e];
+        }
+      }
+      if (XFORM) {
+        float sum = 0.0f;
+        sum = sum + (p[0] + p[4]);
+        sum = sum + (p[1] + p[5]);
+        sum = sum + (p[2] + p[6]);
+        sum = sum + (p[3] + p[7]);
+        for (int i = d8; i < d; i++) {
+          const float x = crow[i];
+          sum = sum + x * x;
+        }
+        cnv = a.squared ? sum : sqrt_rn<float>(sum);
       }
     }
-    const float cv = (METRIC != kMetricDot && col < ns) ? cn[col] : 0.0f;
 #pragma unroll
     for (int r = 0; r < RQ; r++) {
       u64 key = 0ull;
       if (col < ns && row0 + r < m) {
-        const float qv = (METRIC != kMetricDot) ? qn[row0 + r] : 0.0f;
-        const float sc = exact_score<METRIC>(acc[r], qv, cv);
+        const float sc = exact_score<METRIC>(acc[r], XFORM ? qn_s[r] : 0.0f, cnv);
         key = ((u64)okey32(METRIC == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~(uint32_t)col);
       }
       keys[r * 64 * E + col] = key;
@@ -739,48 +842,73 @@ __global__ __launch_bounds__(256) void seed_dots_kernel(const float *__restrict_
   u64 x[E];
 #pragma unroll
   for (int e = 0; e < E; e++) x[e] = keys[w * 64 * E + lane + 64 * e];
-  const u64 th = wave_kth_u64<E>(x, k);
-  if (lane == 0 && th != 0ull) gthr[row] = th - 1;
+  const u64 th = wave_kth_u64<E>(x, a.k);  // nonzero: ns >= k keys, none of them 0
+  if (lane == 0) a.gthr[row] = th ? th - 1 : 0ull;
 }
 
 template <int METRIC>
-static hipError_t launch_seed_dots_t(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int ns,
-                                     int dp, const float *qn, const float *cn, int k, unsigned long long *gthr,
-                                     hipStream_t s) {
+static hipError_t launch_prologue_t(const PrologueArgs &a, unsigned grid, hipStream_t s) {
   using namespace seedk;
-  const unsigned grid = (unsigned)((m + RQ - 1) / RQ);
-  const size_t lds_base = (size_t)RQ * dp * 4;
+  const size_t lds_base = (size_t)RQ * a.dp * 4 + RQ * 4;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void *)seed_dots_kernel<4, METRIC>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)(lds_base + RQ * 256 * 8));
+    hipError_t e = hipFuncSetAttribute((const void *)prologue_kernel<4, METRIC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void *)seed_dots_kernel<8, METRIC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(lds_base + RQ * 512 * 8));
+      e = hipFuncSetAttribute((const void *)prologue_kernel<8, METRIC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void *)seed_dots_kernel<16, METRIC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)(lds_base + RQ * 1024 * 8));
+      e = hipFuncSetAttribute((const void *)prologue_kernel<16, METRIC>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  if (ns <= 256) seed_dots_kernel<4, METRIC><<<grid, 256, lds_base + RQ * 256 * 8, s>>>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr);
-  else if (ns <= 512) seed_dots_kernel<8, METRIC><<<grid, 256, lds_base + RQ * 512 * 8, s>>>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr);
-  else seed_dots_kernel<16, METRIC><<<grid, 256, lds_base + RQ * 1024 * 8, s>>>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr);
+  if (a.ns <= 256) prologue_kernel<4, METRIC><<<grid, 256, lds_base + RQ * 256 * 8, s>>>(a);
+  else if (a.ns <= 512) prologue_kernel<8, METRIC><<<grid, 256, lds_base + RQ * 512 * 8, s>>>(a);
+  else prologue_kernel<16, METRIC><<<grid, 256, lds_base + RQ * 1024 * 8, s>>>(a);
   return hipGetLastError();
 }
 
-hipError_t launch_seed_dots(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int ns, int dp,
-                            const float *qn, const float *cn, int k, int metric, unsigned long long *gthr,
-                            hipStream_t s) {
+hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int64_t n,
+                                  int d, int dp, int ns, int k, int metric, float *qn, float *cn, bool corpus_norms,
+                                  unsigned long long *gthr, void *z0, size_t z0_bytes, void *z1, size_t z1_bytes,
+                                  hipStream_t s) {
   if (m <= 0) return hipSuccess;
-  // the kernel's shapes: whole float4 groups of padded rows, a sample its
-  // LDS holds, 16-byte aligned rows
-  if (ns > kSeedMaxNs || k > ns || dp % 4 != 0 || dp > kSeedDotsMaxD || ldq % 4 != 0 || ldc % 4 != 0 ||
-      ((uintptr_t)q & 15) || ((uintptr_t)c & 15))
+  // the kernel's shapes: whole float4 groups of padded rows, a sample its LDS
+  // holds, 16-byte aligned rows and zeroed ranges
+  if (ns > kSeedMaxNs || k > ns || ns > n || dp % 4 != 0 || dp > kSeedDotsMaxD || d > dp || ldq % 4 != 0 ||
+      ldc % 4 != 0 || (((uintptr_t)q | (uintptr_t)c | (uintptr_t)z0 | (uintptr_t)z1) & 15) || z0_bytes % 16 ||
+      z1_bytes % 16)
     return hipErrorInvalidValue;
-  if (metric == kMetricCosine) return launch_seed_dots_t<kMetricCosine>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr, s);
-  if (metric == kMetricDot) return launch_seed_dots_t<kMetricDot>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr, s);
-  return launch_seed_dots_t<kMetricEuclidean>(q, ldq, m, c, ldc, ns, dp, qn, cn, k, gthr, s);
+  PrologueArgs a{};
+  a.q = q;
+  a.ldq = ldq;
+  a.m = m;
+  a.c = c;
+  a.ldc = ldc;
+  a.n = n;
+  a.d = d;
+  a.dp = dp;
+  a.ns = ns;
+  a.k = k;
+  a.squared = metric == kMetricEuclidean;
+  a.qn = qn;
+  a.cn = cn;
+  a.cinv = cn + n;
+  a.gthr = gthr;
+  a.z0 = (uint4 *)z0;
+  a.z1 = (uint4 *)z1;
+  a.z0n = (int64_t)(z0_bytes / 16);
+  a.z1n = (int64_t)(z1_bytes / 16);
+  a.sblocks = (unsigned)((m + seedk::RQ - 1) / seedk::RQ);
+  const bool xf = metric != kMetricDot;
+  a.qblocks = xf ? (unsigned)((m * 8 + 255) / 256) : 0u;
+  a.cblocks = (xf && corpus_norms) ? (unsigned)((n * 8 + 255) / 256) : 0u;
+  a.zblocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((a.z0n + a.z1n + 255) / 256, 64));
+  const unsigned grid = a.sblocks + a.qblocks + a.cblocks + a.zblocks;
+  if (metric == kMetricCosine) return launch_prologue_t<kMetricCosine>(a, grid, s);
+  if (metric == kMetricDot) return launch_prologue_t<kMetricDot>(a, grid, s);
+  return launch_prologue_t<kMetricEuclidean>(a, grid, s);
 }
 
 hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s) {
