@@ -567,49 +567,13 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
       cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
     }
   };
-  if (LOADER == 0 && a.S <= 64) {
-    // All list lengths in one load (lane s holds list s's), their prefix sum
-    // across the wave, then the row's candidates as ONE flat sequence: slot j
-    // finds its list by a binary search over the prefix sums (lane shuffles)
-    // and MU x 64 slots are loaded at a time.  Short lists (small problems:
-    // a few entries in each of ~30 lists) then cost one round of loads, not
-    // one per list.
-    constexpr int MU = 4;
-    const int nl = (lane < a.S) ? (int)a.cnt[(int64_t)row * a.S + lane] : 0;
-    int incl = nl;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int t = __shfl_up(incl, o, 64);
-      if (lane >= o) incl += t;
-    }
-    const int total = __builtin_amdgcn_readlane(incl, 63);
-    for (int base = 0; base < total; base += 64 * MU) {
-      u64 x[MU];
-#pragma unroll
-      for (int u = 0; u < MU; u++) {
-        const int j = base + 64 * u + lane;
-        // list s: the first with incl_s > j (incl is non-decreasing)
-        int lo = 0, hi = a.S - 1;
-#pragma unroll
-        for (int it = 0; it < 6; it++) {
-          const int mid = (lo + hi) >> 1;
-          const int v = __shfl(incl, mid, 64);
-          if (lo < hi) {
-            if (v > j) hi = mid;
-            else lo = mid + 1;
-          }
-        }
-        const int sj = lo;
-        const int excl = __shfl(incl, sj, 64) - __shfl(nl, sj, 64);
-        x[u] = (j < total) ? a.cand[((int64_t)row * a.S + sj) * a.capg + (j - excl)] : 0ull;
-      }
-#pragma unroll
-      for (int u = 0; u < MU; u++) take(x[u]);
-    }
-  } else if (a.S <= 64) {
-    // (gathered per-rank lists: all the same length) all list lengths in one
-    // load (lane s holds list s's), then the lists' 64-entry chunks as one
-    // flat sequence, MU chunk loads in flight at a time
+  if (a.S <= 64) {
+    // All list lengths in one load (lane s holds list s's), then the lists'
+    // 64-entry chunks as one flat sequence, MU chunk loads in flight at a
+    // time: the row's reads no longer wait on one another (HBM latency, not
+    // bandwidth, bounded the per-list loop).  (A flat per-slot loader -- prefix
+    // sums + a binary search per slot -- measured the same at c1 and 29%
+    // slower at c3.)
     constexpr int MU = 4;
     const int nl = (lane < a.S) ? ((LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + lane] : a.k_in) : 0;
     int s = 0, c = 0;
