@@ -126,6 +126,14 @@ size_t gemm_f32_lds_bytes(int variant, int mode, int capg) {
 #ifndef PMM_F32_KORDER
 #define PMM_F32_KORDER 2
 #endif
+// The 128 x 128 variant (1 wave per SIMD: small problems) uses order 1: at
+// c1 its 32 4-byte DMA issues per wave per K-step were not hidden behind
+// another wave's MFMAs (order 1/3: 0.148 ms per call, order 2: 0.153;
+// tools/experiments/korder_small.sh).  Every order here but 0 is natural,
+// so all variants return the same bits.
+#ifndef PMM_F32_KORDER_SMALL
+#define PMM_F32_KORDER_SMALL 1
+#endif
 
 template <int NB, int NW, int MODE, int METRIC>
 __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a) {
@@ -154,8 +162,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   // a row (physical chunk p>>2, element j = p&3) holds logical chunk
   // ch = (p>>2) ^ swizzle, i.e. k = 8*(ch>>1) + (ch&1) + 2j.  Plain image
   // (16-byte pieces of 1 KiB = 8 rows): chunk ch of a row at ch ^ swizzle.
-  constexpr bool A_GATHER = PMM_F32_KORDER == 2;
-  constexpr bool B_GATHER = PMM_F32_KORDER == 2 || PMM_F32_KORDER == 3;
+  constexpr int KO = (NB == 4 && NW == 4) ? PMM_F32_KORDER_SMALL : PMM_F32_KORDER;
+  constexpr bool A_GATHER = KO == 2;
+  constexpr bool B_GATHER = KO == 2 || KO == 3;
   constexpr int AP = A_GATHER ? 16 : 4, APIECE = A_GATHER ? 256 : 1024, ADW = A_GATHER ? 4 : 16;
   constexpr int BP = B_GATHER ? 4 * G::BPIECES : G::BPIECES, BPIECE = B_GATHER ? 256 : 1024,
                 BDW = B_GATHER ? 4 : 16;
@@ -300,13 +309,13 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           // a plain image (k = 8qd+4h..+3) two v_permlane32_swap trade the
           // lower half's odd k for the upper half's even k, leaving registers
           // {0,2,1,3} = k pairs (8qd,+1) (8qd+2,+3) (8qd+4,+5) (8qd+6,+7).
-          const int co = PMM_F32_KORDER == 0 ? 16 * ((4 * h + qd) ^ swz) : 16 * ((2 * qd + h) ^ swz);
+          const int co = KO == 0 ? 16 * ((4 * h + qd) ^ swz) : 16 * ((2 * qd + h) ^ swz);
           f32x4 av = *(const f32x4 *)(st + a_rd + co);
           f32x4 b[NB];
 #pragma unroll
           for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
-          constexpr bool A_SWAP = PMM_F32_KORDER == 1 || PMM_F32_KORDER == 3;
-          constexpr bool B_SWAP = PMM_F32_KORDER == 1;
+          constexpr bool A_SWAP = KO == 1 || KO == 3;
+          constexpr bool B_SWAP = KO == 1;
           auto kpair = [](f32x4 &x) __attribute__((always_inline)) {
             auto r0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[0]), __float_as_uint(x[1]), false, false);
             auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[2]), __float_as_uint(x[3]), false, false);
