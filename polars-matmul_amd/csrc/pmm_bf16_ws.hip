@@ -7,16 +7,15 @@
 namespace pmm {
 
 size_t gemm_bf16_ws_lds_bytes(int capg, int D) {
-  size_t scr = 0;
+  (void)capg;  // capg <= kBf16WsMaxCapg: compactions select in registers
   switch (D / 128) {
-    case 1: scr = ws::Carve<1>::OFF_SCR; break;
-    case 2: scr = ws::Carve<2>::OFF_SCR; break;
-    case 3: scr = ws::Carve<3>::OFF_SCR; break;
-    case 4: scr = ws::Carve<4>::OFF_SCR; break;
-    case 5: scr = ws::Carve<5>::OFF_SCR; break;
-    default: scr = ws::Carve<6>::OFF_SCR; break;
+    case 1: return ws::Carve<1>::BYTES;
+    case 2: return ws::Carve<2>::BYTES;
+    case 3: return ws::Carve<3>::BYTES;
+    case 4: return ws::Carve<4>::BYTES;
+    case 5: return ws::Carve<5>::BYTES;
+    default: return ws::Carve<6>::BYTES;
   }
-  return scr + (size_t)ws::NWE * capg * 8;
 }
 
 hipError_t launch_bf16_ws_ks1(const GemmF32Args &a, int grid, size_t lds, hipStream_t s);

@@ -77,13 +77,22 @@ constexpr int QCAP = 256;                    // survivor queue per epilogue wave
 // the last barrier of tile t + 1), so one hand-off buffer suffices and its
 // 32 KiB go to the corpus ring: 6 slots = 4 K-steps (64 KiB) in flight per
 // CU, which the L2 / MALL latency needs at ~55 GB/s per CU.
+// Corpus ring slots at KS >= 3 (6 = 4 K-steps, 64 KiB, in flight per CU).
+// The selection-based compaction (capg <= kBf16WsMaxCapg) needs no LDS
+// scratch, so a seventh slot fits (-DPMM_WS_NST=7): measured at c4 it changed
+// nothing (151.0 ms; 121.4 ms without the epilogue, against 121.5 with 6),
+// so the stream is bound by bandwidth, not by the bytes in flight.
+#ifndef PMM_WS_NST
+#define PMM_WS_NST 6
+#endif
 template <int KS>
 struct Carve {
   static constexpr int NHB = KS >= 3 ? 1 : 2;              // hand-off buffers
-  static constexpr int NST = KS >= 3 ? 6 : 4;              // corpus ring slots
+  static constexpr int NST = KS >= 3 ? PMM_WS_NST : 4;     // corpus ring slots
   static constexpr int OFF_RING = OFF_HAND + NHB * NWM * HAND;
   static constexpr int OFF_QUEUE = OFF_RING + NST * STAGE;  // [NWE][QCAP] u64
-  static constexpr int OFF_SCR = OFF_QUEUE + NWE * QCAP * 8;  // [NWE][capg] compaction scratch
+  static constexpr int BYTES = OFF_QUEUE + NWE * QCAP * 8;
+  static_assert(BYTES <= 160 * 1024, "LDS carve");
   static_assert(OFF_RING % 256 == 0 && STAGE % 1024 == 0, "LDS carve alignment");
 };
 static_assert(P * NWE * 1024 == STAGE, "a K-step splits into whole 1 KiB pieces per wave");
@@ -340,7 +349,6 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       float *lo_w = (float *)(smem + OFF_LO) + rw * 32;
       float *cvr = (float *)(smem + OFF_CVR);
       float *cnr = (float *)(smem + OFF_CNR);
-      u64 *scr = (u64 *)(smem + C::OFF_SCR) + (size_t)rw * a.capg;
       if (u.first && lane < 32) {
         const int grow = wrow0 + lane;
         const float qv = (XFORM && grow < a.M) ? a.qn[grow] : 0.0f;
@@ -434,7 +442,8 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             while (need) {
               const int r = __builtin_ctzll(need);
               need &= need - 1;
-              compact_row(a, s, wrow0 + r, thr_w + r, cnt_w + r, scr, lane);
+              // (capg <= 512: compact_row's selection path, no LDS scratch)
+              compact_row(a, s, wrow0 + r, thr_w + r, cnt_w + r, nullptr, lane);
             }
             if (lane < 32) lo_w[lane] = prefilter_bound<METRIC>(thr_w[lane], qex_w[lane]);
             wave_sync();
