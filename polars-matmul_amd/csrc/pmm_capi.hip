@@ -511,6 +511,10 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
   ma.index_base = index_base;
   ma.out_idx = out_idx;
   ma.out_score = out_score;
+  {
+    static const int ablate = getenv("PMM_MERGE_ABLATE") ? atoi(getenv("PMM_MERGE_ABLATE")) : 0;
+    ma.ablate = ablate;
+  }
   Timed t(merge_label, s);
   return launch_merge(ma, 0, s);
 }

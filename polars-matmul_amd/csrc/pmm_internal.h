@@ -70,6 +70,7 @@ struct MergeArgs {
   uint32_t index_base;
   uint32_t *out_idx;
   float *out_score;
+  int ablate;  // benchmarking only (PMM_MERGE_ABLATE): 1 = no selection/sort, 2 = no candidate loads
 };
 
 struct RowSelArgs {

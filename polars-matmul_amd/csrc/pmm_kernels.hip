@@ -576,7 +576,9 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
       cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
     }
   };
-  if (a.S <= 64) {
+  if (a.ablate == 2) {
+    // (benchmarking only: no candidate loads)
+  } else if (a.S <= 64) {
     // All list lengths in one load (lane s holds list s's), then the lists'
     // 64-entry chunks as one flat sequence, MU chunk loads in flight at a
     // time: the row's reads no longer wait on one another (HBM latency, not
@@ -620,11 +622,13 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     }
   }
   wave_sync();
-  if (cnt > a.k_out && a.P <= 512) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
-  const int P2 = min(a.P, next_pow2_dev(cnt));
-  for (int i = cnt + lane; i < P2; i += 64) scr[i] = 0ull;
-  wave_sync();
-  wave_sort_desc_u64(scr, P2, lane);
+  if (a.ablate != 1) {
+    if (cnt > a.k_out && a.P <= 512) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
+    const int P2 = min(a.P, next_pow2_dev(cnt));
+    for (int i = cnt + lane; i < P2; i += 64) scr[i] = 0ull;
+    wave_sync();
+    wave_sort_desc_u64(scr, P2, lane);
+  }
   for (int j = lane; j < a.k_out; j += 64) {
     const u64 x = (j < cnt) ? scr[j] : 0ull;
     uint32_t id = 0xFFFFFFFFu;
