@@ -12,11 +12,12 @@
 // work is split by role, two waves per SIMD:
 //
 //   * 4 MFMA waves (one per SIMD).  Wave w keeps its 32 query rows x D in
-//     AGPRs for a whole work unit (192 registers at D = 768) and streams the
-//     corpus: per 64-column tile, KS K-steps of 128 bf16, each 8 substeps of
-//     two v_mfma_f32_32x32x16_bf16 with the corpus fragments read from LDS
-//     one substep ahead.  After a tile's K-loop it hands its 32 x 64 f32
-//     accumulators to LDS (8 ds_write_b128) and starts the next tile.
+//     registers for a whole work unit (192 registers at D = 768) and streams
+//     the corpus: per 64-column tile, KS K-steps of 128 bf16, each 8 substeps
+//     of two v_mfma_f32_32x32x16_bf16 with the corpus fragments read from LDS
+//     two substeps ahead (across K-step boundaries within a tile).  After a
+//     tile's K-loop it hands its 32 x 64 f32 accumulators to LDS (8
+//     ds_write_b128) and starts the next tile.
 //     No global memory traffic and no epilogue in this role.
 //   * 4 epilogue waves (one per SIMD).  Wave 4 + w owns wave w's 32 rows:
 //     their top-k state (threshold, candidate counts, LDS) has one owner.
@@ -29,14 +30,16 @@
 // s_barriers (the two roles run separate loops with equal trip counts; the
 // per-unit barriers are outside the role branches).  Barrier B_g opens corpus
 // K-step g (ring slot g % NST): before it the epilogue waves have waited
-// (counted vmcnt) for step g's DMA, and the MFMA waves have retired their
-// LDS reads of step g - 1 (lgkmcnt(0)), so after it step g + NST - 1 may be
-// DMA'd into step g - 1's slot.  A tile's accumulators are written before
-// the barrier opening the next tile and read by the epilogue waves after it
-// (double-buffered: tile t + 2 reuses tile t's buffer, written after the
-// epilogue waves have passed the barriers of tile t + 1, by which point they
-// finished with tile t).  The pre-filter column factors and column norms of a
-// tile ride with the tile's first K-step into an 8-tile LDS ring.
+// (counted vmcnt) for the DMA of steps g and g + 1, and the MFMA waves have
+// retired their LDS reads of step g - 1 (counted lgkmcnt: the reads of step
+// g's first substeps, issued during step g - 1, may stay in flight), so after
+// it step g + NST - 1 may be DMA'd into step g - 1's slot.  A tile's
+// accumulators are written before the barrier opening the next tile and read
+// by the epilogue waves after it (double-buffered: tile t + 2 reuses tile t's
+// buffer, written after the epilogue waves have passed the barriers of tile t
+// + 1, by which point they finished with tile t).  The pre-filter column
+// factors and column norms of a tile ride with the tile's first K-step into
+// an 8-tile LDS ring.
 #pragma once
 #include "pmm_device.h"
 
@@ -75,20 +78,20 @@ constexpr int QCAP = 256;                    // survivor queue per epilogue wave
 // epilogue waves are done with tile t's accumulators (read in the first two
 // intervals of tile t + 1) before the MFMA waves write tile t + 1's (after
 // the last barrier of tile t + 1), so one hand-off buffer suffices and its
-// 32 KiB go to the corpus ring: 6 slots = 4 K-steps (64 KiB) in flight per
-// CU, which the L2 / MALL latency needs at ~55 GB/s per CU.
-// Corpus ring slots at KS >= 3 (6 = 4 K-steps, 64 KiB, in flight per CU).
-// The selection-based compaction (capg <= kBf16WsMaxCapg) needs no LDS
-// scratch, so a seventh slot fits (-DPMM_WS_NST=7): measured at c4 it changed
-// nothing (151.0 ms; 121.4 ms without the epilogue, against 121.5 with 6),
-// so the stream is bound by bandwidth, not by the bytes in flight.
+// 32 KiB go to the corpus ring: 7 slots = the step being read, the next
+// (landed: its first fragments are read ahead) and 4 K-steps (64 KiB) in
+// flight per CU, which the L2 / MALL latency needs at ~55 GB/s per CU.
+// (Measured at c4 before the cross-step fragment reads: 5 steps in flight
+// instead of 4 changed nothing, so the stream is bound by bandwidth, not by
+// the bytes in flight.)  The selection-based compaction (capg <=
+// kBf16WsMaxCapg) needs no LDS scratch, which leaves room for the 7th slot.
 #ifndef PMM_WS_NST
-#define PMM_WS_NST 6
+#define PMM_WS_NST 7  // (diagnostic override: -DPMM_WS_NST=n)
 #endif
 template <int KS>
 struct Carve {
   static constexpr int NHB = KS >= 3 ? 1 : 2;              // hand-off buffers
-  static constexpr int NST = KS >= 3 ? PMM_WS_NST : 4;     // corpus ring slots
+  static constexpr int NST = KS >= 3 ? PMM_WS_NST : 5;     // corpus ring slots
   static constexpr int OFF_RING = OFF_HAND + NHB * NWM * HAND;
   static constexpr int OFF_QUEUE = OFF_RING + NST * STAGE;  // [NWE][QCAP] u64
   static constexpr int BYTES = OFF_QUEUE + NWE * QCAP * 8;
@@ -120,6 +123,10 @@ __device__ __forceinline__ void wait_vm_n(int n) {
   }
 }
 __device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(N) : "memory");
+}
 // LDS fetch-and-increment in asm: hipcc waits vmcnt(0) before any LDS write
 // it sees while an LDS-DMA is in flight (it cannot tell the ring from the
 // counters), which would stall the epilogue wave on the ring's next K-steps
@@ -244,7 +251,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
   constexpr bool timing = false;  // (build with -DPMM_WS_STATS for the cycle stats)
 #endif
   const uint64_t t_start = timing ? __builtin_amdgcn_s_memtime() : 0;
-  uint64_t cy0 = 0, cy1 = 0, cy2 = 0, cy3 = 0, nq = 0;
+  uint64_t cy0 = 0, cy1 = 0, cy2 = 0, cy3 = 0, nq = 0, cy4 = 0, cy5 = 0, cy6 = 0, ncomp = 0;
   auto stamp = [&]() __attribute__((always_inline)) { return timing ? __builtin_amdgcn_s_memtime() : 0; };
   if (is_mfma) {
   bf16x8 af[KSUB * KS];  // this wave's query rows, kept across a run's units
@@ -285,38 +292,45 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
         bf16x8 bq[PF + 1][NB];  // fragment sets: PF in flight + the one in use
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
-          wait_lgkm0();  // reads of the previous slot (and the hand-off writes) retired
-          barrier();     // B_g: step g landed
+          const int g0 = KSUB * ks;
+          const int sn = (sl == NST - 1) ? 0 : sl + 1;
+          // reads of the previous slot (and the hand-off writes) retired; the
+          // PF groups prefetched from this slot may stay in flight
+          if (ks == 0) wait_lgkm0();
+          else wait_lgkm<PF * NB>();
+          barrier();     // B_g: steps g and g + 1 landed
           uint32_t sbase = ring_lds + (uint32_t)(sl * STAGE) + lane_off;
           asm volatile("" : "+v"(sbase));  // keep the per-substep XORs in the loop
-          auto rd = [&](int sub, int set) __attribute__((always_inline)) {
-            const uint32_t ad = sbase ^ (uint32_t)(sub << 4);
+          auto rd = [&](uint32_t base, int sub, int set) __attribute__((always_inline)) {
+#ifdef PMM_WS_NOFRAG
+            return;  // diagnostic build only: MFMAs on stale fragments, no LDS reads
+#endif
+            const uint32_t ad = base ^ (uint32_t)(sub << 4);
 #pragma unroll
             for (int c = 0; c < NB; c++) bq[set][c] = *(const LDS_AS bf16x8 *)(size_t)(ad + c * 32 * KB);
           };
-          const int g0 = KSUB * ks;
+          // fragments stream PF substeps ahead across the K-steps of a tile:
+          // step g + 1's slot landed before B_g, so its first PF substeps are
+          // read during step g and the barrier costs no read latency
+          uint32_t nbase = ring_lds + (uint32_t)(sn * STAGE) + lane_off;
+          asm volatile("" : "+v"(nbase));
+          if (ks == 0) {
 #pragma unroll
-          for (int p = 0; p < PF; p++) rd(p, (g0 + p) % (PF + 1));
-          // the previous step's last MFMA group, held back past the barrier:
-          // it covers the latency of the reads just issued
-          if (ks > 0) {
-#pragma unroll
-            for (int c = 0; c < NB; c++) mfma_acc(acc[c], af[g0 - 1], bq[(g0 - 1) % (PF + 1)][c]);
+            for (int p = 0; p < PF; p++) rd(sbase, p, p % (PF + 1));
           }
 #pragma unroll
           for (int sub = 0; sub < KSUB; sub++) {
             const int gs = g0 + sub;
-            if (sub + PF < KSUB) rd(sub + PF, (gs + PF) % (PF + 1));
-            if (!(sub == KSUB - 1 && ks < KS - 1)) {
+            if (sub + PF < KSUB) rd(sbase, sub + PF, (gs + PF) % (PF + 1));
+            else if (ks < KS - 1) rd(nbase, sub + PF - KSUB, (gs + PF) % (PF + 1));
 #pragma unroll
-              for (int c = 0; c < NB; c++) {
-                if (gs == 0) mfma_first(acc[c], af[0], bq[0][c]);
-                else mfma_acc(acc[c], af[gs], bq[gs % (PF + 1)][c]);
-              }
+            for (int c = 0; c < NB; c++) {
+              if (gs == 0) mfma_first(acc[c], af[0], bq[0][c]);
+              else mfma_acc(acc[c], af[gs], bq[gs % (PF + 1)][c]);
             }
             __builtin_amdgcn_sched_barrier(0);
           }
-          sl = (sl == NST - 1) ? 0 : sl + 1;
+          sl = sn;
         }
         mfma_drain(acc);
         // hand the tile to the epilogue wave of these rows
@@ -415,6 +429,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       const u64 *lq = (const u64 *)(smem + C::OFF_QUEUE) + rw * QCAP;
       int qlen = 0;  // wave-uniform
       auto drain = [&]() __attribute__((always_inline)) {
+        const uint64_t td0 = stamp();
         if (timing) nq += (uint64_t)qlen;
         for (int base = 0; base < qlen; base += 64) {
           const int i = base + lane;
@@ -438,6 +453,8 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
           const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
           u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 64));
           if (need) {
+            const uint64_t tc0 = stamp();
+            if (timing) ncomp += (uint64_t)__popcll(need);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             while (need) {
               const int r = __builtin_ctzll(need);
@@ -448,9 +465,11 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             if (lane < 32) lo_w[lane] = prefilter_bound<METRIC>(thr_w[lane], qex_w[lane]);
             wave_sync();
             load_lo();
+            if (timing) cy4 += stamp() - tc0;
           }
         }
         qlen = 0;
+        if (timing) cy6 += stamp() - td0;
       };
 
       // epilogue of column group c of tile pt (accumulators in hand-off
@@ -464,6 +483,10 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
         for (int q = 0; q < 4; q++) v4[q] = *(const f32x4 *)(hb + ((c * 4 + q) * 64 + lane) * 16);
         const int tc = 32 * c + r32;
         const int gcol = pt * BN + tc;
+        if (a.ablate & 32) {  // benchmarking only: the hand-off reads, nothing else
+          asm volatile("" ::"v"(v4[0]), "v"(v4[1]), "v"(v4[2]), "v"(v4[3]));
+          return;
+        }
         const float cv = XFORM ? cvr[(pt & (CVT - 1)) * BN + tc] : 0.0f;
         float d[16];
 #pragma unroll
@@ -472,7 +495,8 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
 #pragma unroll
         for (int e = 1; e < 16; e++) dm = __builtin_elementwise_maximum(dm, d[e]);
         const bool any = !(dm < 0.0f) && gcol < a.N;
-        if (__ballot(any) == 0ull) return;
+        if (__ballot(any) == 0ull || (a.ablate & 8)) return;  // (8: benchmarking, pre-filter only)
+        const uint64_t tq0 = stamp();
         uint32_t bits = 0u;
 #pragma unroll
         for (int e = 0; e < 16; e++) bits = (bits << 1) | (uint32_t)!(d[e] < 0.0f);
@@ -499,19 +523,25 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             drain();
           }
         }
+        if (timing) cy5 += stamp() - tq0;
       };
 
-      // prologue: K-steps 0 .. NST-2 of the unit; step 0 landed before B_0
+      // prologue: K-steps 0 .. NST-2 of the unit; steps 0 and 1 landed
+      // before B_0 (the MFMA waves read step g + 1's first fragments in step g)
+      constexpr int LEAD = 1;
 #pragma unroll
       for (int j = 0; j < NST - 1; j++) stage(j, t0 + j / KS, j % KS);
       {
         int n = 0;
 #pragma unroll
-        for (int j = 1; j < NST - 1; j++) n += step_dmas<XFORM>(j % KS);
+        for (int j = 1 + LEAD; j < NST - 1; j++) n += step_dmas<XFORM>(j % KS);
         wait_vm_n(n);
       }
       int sl = 0;
       for (int tile = t0; tile < t1; tile++) {
+        // unrolled: compile-time slot / count arithmetic (a runtime K-step
+        // loop, 40% less code, measured 12% slower at c4: the epilogue waves'
+        // per-interval instructions are on the critical path)
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
           uint64_t tt = stamp();
@@ -558,11 +588,11 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             cy1 += t2 - tt;
             tt = t2;
           }
-          // step g + 1 landed; steps g + 2 .. g + NST - 1 may stay in flight
+          // step g + 1 + LEAD landed; later steps may stay in flight
           {
             int n = 0;
 #pragma unroll
-            for (int j = 2; j < NST; j++) n += step_dmas<XFORM>((ks + j) % KS);
+            for (int j = 2 + LEAD; j < NST; j++) n += step_dmas<XFORM>((ks + j) % KS);
             wait_vm_n(n);
           }
           if (timing) cy2 += stamp() - tt;
@@ -585,8 +615,10 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
     }
   }
   if (timing && lane == 0) {
-    // MFMA waves: [0] cycles at barriers, [1] all; epilogue waves: [3] DMA
-    // issue, [4] epilogue, [5] vmcnt waits, [6] barriers, [7] all
+    // MFMA waves: [1] all; epilogue waves: [0] survivors queued, [3] DMA
+    // issue, [4] epilogue, [5] vmcnt waits, [6] barriers, [7] all, [8]
+    // compactions, [9] rows compacted, [10] survivor queueing (incl. drains
+    // it triggers), [11] drains (incl. compactions)
     const uint64_t all = __builtin_amdgcn_s_memtime() - t_start;
     if (is_mfma) {
       atomicAdd(a.stats + 1, (u64)all);  // (no per-phase stamps: the role has no spare registers)
@@ -597,6 +629,10 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       atomicAdd(a.stats + 5, (u64)cy2);
       atomicAdd(a.stats + 6, (u64)cy3);
       atomicAdd(a.stats + 7, (u64)all);
+      atomicAdd(a.stats + 8, (u64)cy4);
+      atomicAdd(a.stats + 9, (u64)ncomp);
+      atomicAdd(a.stats + 10, (u64)cy5);
+      atomicAdd(a.stats + 11, (u64)cy6);
     }
   }
 }

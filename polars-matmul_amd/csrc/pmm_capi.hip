@@ -744,8 +744,8 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     static const bool stats = getenv("PMM_STATS") != nullptr;
     static unsigned long long *stats_buf = nullptr;
     if (stats) {
-      if (!stats_buf) HIP_TRY(hipMalloc(&stats_buf, 64));
-      HIP_TRY(hipMemsetAsync(stats_buf, 0, 64, s));
+      if (!stats_buf) HIP_TRY(hipMalloc(&stats_buf, 128));
+      HIP_TRY(hipMemsetAsync(stats_buf, 0, 128, s));
       a.stats = stats_buf;
     }
     {
@@ -755,16 +755,18 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
                                 : launch_gemm_bf16(a, p.grid, s));
     }
     if (stats) {
-      unsigned long long h[8];
-      HIP_TRY(hipMemcpyAsync(h, stats_buf, 64, hipMemcpyDeviceToHost, s));
+      unsigned long long h[16];
+      HIP_TRY(hipMemcpyAsync(h, stats_buf, 128, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
       if (p.variant == -2)
         fprintf(stderr,
                 "[pmm stats] gemm_bf16_ws: units %d, S %d, tps %d, sync timeouts %llu, survivors "
                 "%llu; MFMA-wave cycles %.3g; epilogue-wave cycles: DMA issue %.3g, epilogue "
-                "%.3g, vmcnt waits %.3g, barriers %.3g of %.3g\n",
+                "%.3g, vmcnt waits %.3g, barriers %.3g of %.3g; compactions %.3g (%llu rows), "
+                "survivor queueing %.3g, drains %.3g\n",
                 p.units, p.S, p.tps, h[2], h[0], (double)h[1], (double)h[3], (double)h[4],
-                (double)h[5], (double)h[6], (double)h[7]);
+                (double)h[5], (double)h[6], (double)h[7], (double)h[8], h[9], (double)h[10],
+                (double)h[11]);
       else
       fprintf(stderr,
               "[pmm stats] gemm_bf16: queued %llu, LDS-queue tiles %llu, sync timeouts %llu, "
