@@ -282,7 +282,8 @@ def timed_steps(runner, steps, warmup, dist):
 def kernel_stats(bf16):
     from polars_matmul import _native
 
-    names = {"gemm": "gemm_bf16_topk" if bf16 else "gemm_f32_topk", "seed": "gemm_f32_seed",
+    names = {"gemm": "gemm_bf16_topk" if bf16 else "gemm_f32_topk",
+             "seed": "seed_bf16" if bf16 else "gemm_f32_seed",
              "merge": "merge_topk", "shard_merge": "merge_shards", "norms": "norms_"}
     out = {}
     for key, nm in names.items():

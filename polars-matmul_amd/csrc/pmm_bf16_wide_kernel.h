@@ -387,7 +387,7 @@ __global__ __launch_bounds__(wd::NTH, 1) void gemm_bf16_wide_kernel(GemmF32Args 
       constexpr int g0 = KSI * KSUB;
       static_assert(PF == 1 && KSUB % 2 == 0, "fragment rotation");
       frag_read(cf[0], sb);
-      if (KSI > 0) mfma_acc(acc, cf[1], qf[g0 - 1]);
+      if constexpr (KSI > 0) mfma_acc(acc, cf[1], qf[g0 - 1]);
 #pragma unroll
       for (int sub = 0; sub < KSUB; sub++) {
         const int gs = g0 + sub;

@@ -25,6 +25,27 @@ hipError_t launch_bf16_ws_ks4(const GemmF32Args &a, int grid, size_t lds, hipStr
 hipError_t launch_bf16_ws_ks5(const GemmF32Args &a, int grid, size_t lds, hipStream_t s);
 hipError_t launch_bf16_ws_ks6(const GemmF32Args &a, int grid, size_t lds, hipStream_t s);
 
+hipError_t launch_seed_bf16_ws_ks1(const GemmF32Args &a, float *S, int ns, hipStream_t s);
+hipError_t launch_seed_bf16_ws_ks2(const GemmF32Args &a, float *S, int ns, hipStream_t s);
+hipError_t launch_seed_bf16_ws_ks3(const GemmF32Args &a, float *S, int ns, hipStream_t s);
+hipError_t launch_seed_bf16_ws_ks4(const GemmF32Args &a, float *S, int ns, hipStream_t s);
+hipError_t launch_seed_bf16_ws_ks5(const GemmF32Args &a, float *S, int ns, hipStream_t s);
+hipError_t launch_seed_bf16_ws_ks6(const GemmF32Args &a, float *S, int ns, hipStream_t s);
+
+hipError_t launch_seed_bf16_ws(const GemmF32Args &a, float *S, int ns, hipStream_t s) {
+  // whole 32-column sample tiles inside the corpus, whole K-steps
+  if (ns < 32 || ns % 32 != 0 || ns > a.N || a.D % kBf16DAlign != 0 || a.M <= 0) return hipErrorInvalidValue;
+  switch (a.D / 128) {
+    case 1: return launch_seed_bf16_ws_ks1(a, S, ns, s);
+    case 2: return launch_seed_bf16_ws_ks2(a, S, ns, s);
+    case 3: return launch_seed_bf16_ws_ks3(a, S, ns, s);
+    case 4: return launch_seed_bf16_ws_ks4(a, S, ns, s);
+    case 5: return launch_seed_bf16_ws_ks5(a, S, ns, s);
+    case 6: return launch_seed_bf16_ws_ks6(a, S, ns, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 hipError_t launch_gemm_bf16_ws(const GemmF32Args &a, int grid, hipStream_t s) {
   const size_t lds = gemm_bf16_ws_lds_bytes(a.capg, a.D);
   // the kernel's grid and tile shapes assume: whole 128-wide K-steps, a

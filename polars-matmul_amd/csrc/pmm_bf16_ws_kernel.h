@@ -637,6 +637,84 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
   }
 }
 
+// ===========================================================================
+// Threshold seed for the wave-specialised kernel.  The scores of the first ns
+// corpus rows, computed the way the main pass computes them -- the same query
+// fragments (registers), the same corpus K-chunk per lane and substep, the
+// same chain of v_mfma_f32_32x32x16_bf16 per 32-column block from
+// mfma_first, the same exact_score on the same norms -- so each is bit for
+// bit the score the main pass gives that (row, column).  Stored S[row][col]
+// (the main pass's candidate buffers, unused until it starts) for
+// seed_select_kernel, which sets gthr[row] = (k-th best composite) - 1: an
+// exact lower bound of the row's final k-th best.  The corpus fragments come
+// straight from global memory (the sample is a few MB, L2-resident); one wave
+// per 32 query rows, one workgroup per 128.  (The first MFMA accumulates onto
+// zeros where the main pass's uses the inline constant 0: the same sums.)
+// ===========================================================================
+template <int KS, int METRIC>
+__global__ __launch_bounds__(256, 1) void seed_bf16_ws_kernel(GemmF32Args a, float *__restrict__ S, int ns) {
+  using namespace ws;
+  constexpr int G = KSUB * KS;  // K substeps of 16
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int r32 = lane & 31, h = lane >> 5;
+  const int wrow0 = (int)blockIdx.x * BM + w * 32;
+  if (wrow0 >= a.M) return;  // (wave-uniform)
+  bf16x8 af[G];
+  {
+    const __amdgpu_buffer_rsrc_t rq =
+        make_rsrc(a.qb + (int64_t)wrow0 * a.ldq, (int64_t)min(32, a.M - wrow0) * a.ldq * 2);
+    const uint32_t qoff = (uint32_t)(r32 * a.ldq * 2 + 128 * h);
+    // (compiler-visible loads: these registers may be moved before use, and
+    // an asm load's destination must not be read before its wait)
+#pragma unroll
+    for (int i = 0; i < G; i++)
+      af[i] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, (int)(qoff + ((i / KSUB) * 128 + (i % KSUB) * 8) * 2), 0, 0));
+  }
+  constexpr bool XFORM = METRIC != kMetricDot;
+  float qv[16];
+#pragma unroll
+  for (int e = 0; e < 16; e++) {
+    const int row = wrow0 + acc_row(e, h);
+    qv[e] = (XFORM && row < a.M) ? a.qn[row] : 0.0f;
+  }
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(a.cb, (int64_t)ns * a.ldc * 2);
+  for (int t = 0; t < ns / 32; t++) {
+    const int col = t * 32 + r32;
+    // lane (r32, h), substep gs: column col, K-step gs / 8, chunk 8h + gs % 8
+    const uint32_t boff = (uint32_t)(col * a.ldc * 2 + 128 * h);
+    bf16x8 b[G];
+#pragma unroll
+    for (int gs = 0; gs < G; gs++)
+      b[gs] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rc, (int)(boff + ((gs / KSUB) * 128 + (gs % KSUB) * 8) * 2),
+                                                        0, 0));
+    __builtin_amdgcn_sched_barrier(0);  // all of the tile's loads in flight before its MFMAs
+    // the compiler's MFMA builtin (the same instruction as the main pass's
+    // asm, so the same bits): here hipcc allocates the operands freely and
+    // must see the instruction to pad its register hazards
+    typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
+    f32x16 acc = {};
+#pragma unroll
+    for (int gs = 0; gs < G; gs++)
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16v8, af[gs]),
+                                                    __builtin_bit_cast(bf16v8, b[gs]), acc, 0, 0, 0);
+    const float cv = XFORM ? a.cn[col] : 0.0f;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      const int row = wrow0 + acc_row(e, h);
+      if (row < a.M) S[(int64_t)row * ns + col] = exact_score<METRIC>(acc[e], qv[e], cv);
+    }
+  }
+}
+
+template <int KS, int METRIC>
+static hipError_t launch_seed_bf16_ws_t(const GemmF32Args &a, float *S, int ns, hipStream_t s) {
+  seed_bf16_ws_kernel<KS, METRIC><<<dim3((unsigned)((a.M + ws::BM - 1) / ws::BM)), dim3(256), 0, s>>>(a, S, ns);
+  return hipGetLastError();
+}
+
 template <int KS, int METRIC>
 static hipError_t launch_bf16_ws_t(const GemmF32Args &a, int grid, size_t lds, hipStream_t s) {
   static bool attr_set = false;

@@ -17,4 +17,11 @@ hipError_t PMM_CAT(launch_bf16_ws_ks, PMM_BF16_KS)(const GemmF32Args &a, int gri
   return launch_bf16_ws_t<PMM_BF16_KS, kMetricEuclidean>(a, grid, lds, s);
 }
 
+hipError_t PMM_CAT(launch_seed_bf16_ws_ks, PMM_BF16_KS)(const GemmF32Args &a, float *S, int ns,
+                                                       hipStream_t s) {
+  if (a.metric == kMetricCosine) return launch_seed_bf16_ws_t<PMM_BF16_KS, kMetricCosine>(a, S, ns, s);
+  if (a.metric == kMetricDot) return launch_seed_bf16_ws_t<PMM_BF16_KS, kMetricDot>(a, S, ns, s);
+  return launch_seed_bf16_ws_t<PMM_BF16_KS, kMetricEuclidean>(a, S, ns, s);
+}
+
 }  // namespace pmm

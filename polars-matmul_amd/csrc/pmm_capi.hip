@@ -749,6 +749,24 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
       a.stats = stats_buf;
     }
     {
+      // Threshold seed (wave-specialised kernel): unseeded, every row starts
+      // at "accept all" and its threshold only rises at compactions (every
+      // ~220 appends), so a row queues and re-scores ~2k survivors over a 1M
+      // corpus.  The k-th best of the first ns columns -- scored bit for bit
+      // as the main pass scores them -- minus 1 is an exact lower bound of
+      // the row's final k-th best: the main pass starts from it.
+      const int seed_env = getenv("PMM_BF16_SEED") ? atoi(getenv("PMM_BF16_SEED")) : 1;  // (read per call: tests toggle it)
+      int64_t ns = kSeedMaxNs;
+      if (const char *ne = getenv("PMM_SEED_NS")) ns = std::max<int64_t>(32, std::min<int64_t>(atoll(ne), kSeedMaxNs) / 32 * 32);
+      if (seed_env && p.variant == -2 && 4 * k <= ns && n >= 8 * ns &&
+          (size_t)m * ns * 4 <= p.off_qn - p.off_cand) {
+        float *sample = (float *)(w + p.off_cand);
+        Timed t("seed_bf16", s);
+        HIP_TRY(launch_seed_bf16_ws(a, sample, (int)ns, s));
+        HIP_TRY(launch_seed_select(sample, ns, (int)m, (int)ns, (int)k, metric, a.gthr, s));
+      }
+    }
+    {
       Timed t("gemm_bf16_topk", s);
       HIP_TRY(p.variant == -3   ? launch_gemm_bf16_wide(a, p.grid, s)
               : p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s)

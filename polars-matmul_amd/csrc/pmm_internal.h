@@ -130,6 +130,9 @@ constexpr int kBf16WsBN = 64;
 constexpr int kBf16WsMaxCapg = 512;
 size_t gemm_bf16_ws_lds_bytes(int capg, int D);  // D = padded dimension
 hipError_t launch_gemm_bf16_ws(const GemmF32Args &a, int grid, hipStream_t s);
+// bf16 threshold seed (pmm_bf16_ws_kernel.h): S[row][0..ns) = the scores of
+// corpus rows 0..ns-1 exactly as the wave-specialised kernel computes them
+hipError_t launch_seed_bf16_ws(const GemmF32Args &a, float *S, int ns, hipStream_t s);
 // 256-query-row bf16 kernel (pmm_bf16_wide_kernel.h): 8 waves (2 per SIMD),
 // each 32 query rows x D in registers, 32-column corpus tiles; used when capg
 // <= kBf16WideMaxCapg unless PMM_BF16_WIDE=0.

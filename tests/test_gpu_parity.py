@@ -620,6 +620,32 @@ def test_bf16_wide_equals_wave_specialised(pmm, m, n, d, k, metric, monkeypatch)
     assert np.array_equal(gs, ws_)
 
 
+@pytest.mark.parametrize("m,n,d", [(300, 20000, 768), (140, 9000, 200)])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_seeded_threshold_is_exact(pmm, m, n, d, metric, monkeypatch):
+    # the wave-specialised kernel starts each row from the k-th best of the
+    # first ns columns (seed_bf16_ws_kernel + seed_select_kernel): those
+    # scores are bit-identical to the main pass's, so the seed is an exact
+    # lower bound and the lists equal the unseeded run's bit for bit --
+    # including exact ties inside and across the sample
+    rs = np.random.RandomState(m + n + d)
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    c[5000:5040] = c[:40]        # sample columns duplicated past the sample
+    c[300:310] = c[700:710]      # duplicates inside the sample
+    q[7] = c[3]                  # a query equal to a sample column
+    for k, ns in ((1, None), (10, None), (100, None), (256, None), (10, "64"), (50, "512")):
+        monkeypatch.setenv("PMM_BF16_SEED", "0")
+        want = gpu_topk_bf16(q, c, k, metric)
+        monkeypatch.setenv("PMM_BF16_SEED", "1")
+        if ns:
+            monkeypatch.setenv("PMM_SEED_NS", ns)
+        got = gpu_topk_bf16(q, c, k, metric)
+        monkeypatch.delenv("PMM_SEED_NS", raising=False)
+        assert np.array_equal(got[0], want[0]), (metric, k, ns, float(np.mean(got[0] == want[0])))
+        assert np.array_equal(got[1].view(np.uint32), want[1].view(np.uint32)), (metric, k, ns)
+
+
 def test_bf16_recall_vs_f32(pmm):
     # SURVEY 8c bf16 criterion: recall@k >= 0.95 against the f32 result
     rs = np.random.RandomState(31)
