@@ -22,6 +22,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace pmm {
 
 hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld, int squared,
@@ -76,6 +78,10 @@ hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld
 // the K loop), so each output is the k-ordered fmaf chain of the oracle
 // bit for bit (v_mfma_f32_32x32x2_f32 is an exact f32 FMA chain).
 // ===========================================================================
+#ifndef PMM_F32_DEFER
+#define PMM_F32_DEFER 1
+#endif
+
 template <int NB, int NW>
 struct GemmShape {
   static constexpr int BN = 32 * NB;                // corpus columns per tile
@@ -296,7 +302,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       f32x16 acc[NB];
 #pragma unroll
       for (int c = 0; c < NB; c++) acc[c] = (f32x16){};
-      for (int ks = 0; ks < KS; ks++) {
+      // PMM_F32_DEFER: the last substep(s) of a K step (NB MFMAs each, their
+      // operands one A and NB B values) run after the next step's barrier,
+      // behind the next step's first fragment reads -- the same MFMA order
+      // per accumulator, so the same bits
+      constexpr int DN = PMM_F32_DEFER;  // substeps deferred (1 or 2)
+      static_assert(DN >= 0 && DN <= 2, "PMM_F32_DEFER: 0, 1 or 2 substeps");
+      float dA[DN > 0 ? DN : 1], dB[DN > 0 ? DN : 1][NB];
+      // one K step; DEF: defer its last substep, PREV: run the previous
+      // step's deferred substep first (compile-time, so no per-substep branch)
+      auto kstep = [&](int ks, auto DEF, auto PREV) __attribute__((always_inline)) {
         __syncthreads();  // stage `buf` landed (vmcnt(0) + barrier); buf^1 free
         const char *st = smem + buf * G::STAGE;
 #pragma unroll
@@ -324,6 +339,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             x[2] = __uint_as_float(r1[0]);
             x[3] = __uint_as_float(r1[1]);
           };
+          if (decltype(PREV)::value && qd == 0) {
+            // the previous step's deferred substeps, behind this step's reads
+#pragma unroll
+            for (int j = 0; j < DN; j++)
+#pragma unroll
+              for (int c = 0; c < NB; c++)
+                acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(dA[j], dB[j][c], acc[c], 0, 0, 0);
+          }
           if (A_SWAP) kpair(av);
 #pragma unroll
           for (int c = 0; c < NB; c++)
@@ -332,9 +355,15 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           for (int jj = 0; jj < 4; jj++) {
             const int js = ((jj & 1) << 1) | (jj >> 1);  // swapped registers: {0, 2, 1, 3}
             const int ja = A_SWAP ? js : jj, jb = B_SWAP ? js : jj;
+            if (decltype(DEF)::value && qd == 3 && jj >= 4 - DN) {
+              dA[jj - (4 - DN)] = av[ja];
 #pragma unroll
-            for (int c = 0; c < NB; c++)
-              acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ja], b[c][jb], acc[c], 0, 0, 0);
+              for (int c = 0; c < NB; c++) dB[jj - (4 - DN)][c] = b[c][jb];
+            } else {
+#pragma unroll
+              for (int c = 0; c < NB; c++)
+                acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ja], b[c][jb], acc[c], 0, 0, 0);
+            }
           }
           if (qd < NPART) {
             // next step's LDS-DMA goes out behind the MFMA groups, so the
@@ -347,6 +376,15 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           }
         }
         buf ^= 1;
+      };
+      using Yes = std::integral_constant<bool, true>;
+      using No = std::integral_constant<bool, false>;
+      if (!PMM_F32_DEFER || KS == 1) {
+        for (int ks = 0; ks < KS; ks++) kstep(ks, No{}, No{});
+      } else {
+        kstep(0, Yes{}, No{});
+        for (int ks = 1; ks + 1 < KS; ks++) kstep(ks, Yes{}, Yes{});
+        kstep(KS - 1, No{}, Yes{});
       }
       rb = rbn;
 
