@@ -620,7 +620,8 @@ def test_bf16_wide_equals_wave_specialised(pmm, m, n, d, k, metric, monkeypatch)
     assert np.array_equal(gs, ws_)
 
 
-@pytest.mark.parametrize("m,n,d", [(300, 20000, 768), (140, 9000, 200)])
+@pytest.mark.parametrize("m,n,d", [(300, 20000, 768), (140, 9000, 200), (70, 8200, 128), (64, 8500, 384),
+                                   (100, 9100, 512), (129, 8300, 640)])
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
 def test_bf16_seeded_threshold_is_exact(pmm, m, n, d, metric, monkeypatch):
     # the wave-specialised kernel starts each row from the k-th best of the
