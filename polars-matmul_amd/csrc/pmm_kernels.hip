@@ -811,21 +811,39 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     if (col < ns) {
       const float *crow = a.c + (int64_t)col * a.ldc;
       const f32x4 *cr = (const f32x4 *)crow;
-      for (int j4 = 0; j4 < dp / 4; j4++) {
-        const f32x4 cv = cr[j4];
+      // the row's 16-byte pieces stream through a ring of PD loads in flight
+      // (one at a time, each load's latency was exposed: 64 per row at D =
+      // 256); the arithmetic and its order are unchanged
+      // (dp is a multiple of 32, so nj a multiple of PD; loads past the row's
+      // end re-read its last piece, so every load is unconditional and the
+      // compiler counts its waits)
+      constexpr int PD = 8;  // (measured at c1: 16 and 2-row blocks both slower)
+      const int nj = dp / 4;
+      f32x4 ring[PD];
 #pragma unroll
-        for (int r = 0; r < RQ; r++) {
-          const f32x4 q4 = *(const f32x4 *)(qs + r * dp + 4 * j4);  // broadcast
-          acc[r] = fmaf(q4[0], cv[0], acc[r]);
-          acc[r] = fmaf(q4[1], cv[1], acc[r]);
-          acc[r] = fmaf(q4[2], cv[2], acc[r]);
-          acc[r] = fmaf(q4[3], cv[3], acc[r]);
-        }
-        if (XFORM && 4 * j4 < d8) {
-          // ndarray order: accumulator j sums x[8t + j]^2 over t
-          const int o = (j4 & 1) * 4;
+      for (int q = 0; q < PD; q++) ring[q] = cr[min(q, nj - 1)];
+      for (int j0 = 0; j0 < nj; j0 += PD) {
 #pragma unroll
-          for (int e = 0; e < 4; e++) p[o + e] = p[o + e] + cv[e] * cv[e];
+        for (int q = 0; q < PD; q++) {
+          const int j4 = j0 + q;
+          {
+            const f32x4 cv = ring[q];
+            ring[q] = cr[min(j4 + PD, nj - 1)];
+#pragma unroll
+            for (int r = 0; r < RQ; r++) {
+              const f32x4 q4 = *(const f32x4 *)(qs + r * dp + 4 * j4);  // broadcast
+              acc[r] = fmaf(q4[0], cv[0], acc[r]);
+              acc[r] = fmaf(q4[1], cv[1], acc[r]);
+              acc[r] = fmaf(q4[2], cv[2], acc[r]);
+              acc[r] = fmaf(q4[3], cv[3], acc[r]);
+            }
+            if (XFORM && 4 * j4 < d8) {
+              // ndarray order: accumulator j sums x[8t + j]^2 over t
+              const int o = (j4 & 1) * 4;
+#pragma unroll
+              for (int e = 0; e < 4; e++) p[o + e] = p[o + e] + cv[e] * cv[e];
+            }
+          }
         }
       }
       if (XFORM) {
@@ -891,7 +909,7 @@ hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const floa
   if (m <= 0) return hipSuccess;
   // the kernel's shapes: whole float4 groups of padded rows, a sample its LDS
   // holds, 16-byte aligned rows and zeroed ranges
-  if (ns > kSeedMaxNs || k > ns || ns > n || dp % 4 != 0 || dp > kSeedDotsMaxD || d > dp || ldq % 4 != 0 ||
+  if (ns > kSeedMaxNs || k > ns || ns > n || dp % 32 != 0 || dp > kSeedDotsMaxD || d > dp || ldq % 4 != 0 ||
       ldc % 4 != 0 || (((uintptr_t)q | (uintptr_t)c | (uintptr_t)z0 | (uintptr_t)z1) & 15) || z0_bytes % 16 ||
       z1_bytes % 16)
     return hipErrorInvalidValue;
