@@ -623,7 +623,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     // bandwidth, bounded the per-list loop).  (A flat per-slot loader -- prefix
     // sums + a binary search per slot -- measured the same at c1 and 29%
     // slower at c3.)
-    constexpr int MU = 4;
+    constexpr int MU = 4;  // (8 and 16 in flight measured the same at c1 and c3)
     const int nl = (lane < a.S) ? ((LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + lane] : a.k_in) : 0;
     int s = 0, c = 0;
     int ns = __builtin_amdgcn_readlane(nl, 0);
