@@ -635,6 +635,9 @@ def test_bf16_seeded_threshold_is_exact(pmm, m, n, d, metric, monkeypatch):
     c[5000:5040] = c[:40]        # sample columns duplicated past the sample
     c[300:310] = c[700:710]      # duplicates inside the sample
     q[7] = c[3]                  # a query equal to a sample column
+    c[100, 5] = np.nan           # NaN scores inside the sample ...
+    c[n - 3, 0] = np.nan         # ... and past it
+    q[11, 2] = np.nan            # a query row whose every score is NaN
     for k, ns in ((1, None), (10, None), (100, None), (256, None), (10, "64"), (50, "512")):
         monkeypatch.setenv("PMM_BF16_SEED", "0")
         want = gpu_topk_bf16(q, c, k, metric)
