@@ -371,7 +371,9 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8):
     ach = flops / (all_gemm_ms / 1000.0) / 1e12 if gemm_ms else None
     roof = {
         "bound": "mfma",
-        "kernel": f"gemm_{cdt}_kernel (fused GEMM + metric + top-k)",
+        "kernel": ("gemm_bf16_ws_kernel (wave-specialised fused GEMM + metric + top-k; "
+                   "+ seed_bf16_ws_kernel in achieved)" if bf16 else
+                   "gemm_f32_kernel (fused GEMM + metric + top-k)"),
         "achieved": round(ach, 2) if ach else None,
         "peak": peak, "unit": "TFLOP/s",
         "frac": round(ach / peak, 4) if ach else None,
