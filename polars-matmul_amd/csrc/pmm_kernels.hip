@@ -288,11 +288,17 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     // one, TP / NPART pieces each (the natural-order image takes 4x the
     // pieces of the 16-byte form; spread, they do not stall one group)
     constexpr int TP = AP + BP;
-#ifdef PMM_F32_DMA_PARTS
-    constexpr int NPART = PMM_F32_DMA_PARTS;  // (A/B: 4 measured 7% slower at c3)
-#else
-    constexpr int NPART = 1;
+#ifndef PMM_F32_DMA_PARTS
+#define PMM_F32_DMA_PARTS 1  // (A/B: 4 measured 7% slower at c3)
 #endif
+#ifndef PMM_F32_DMA_PARTS_SMALL
+#define PMM_F32_DMA_PARTS_SMALL 2
+#endif
+    // (the 128 x 128 variant runs one wave per SIMD: no second wave's MFMAs
+    // cover this wave's DMA issue; its 8 pieces per step go out 4 behind each
+    // of the first two MFMA groups: c1 0.141 vs 0.143 ms, c2 0.134 vs 0.136;
+    // 2 behind each of four groups 0.146 / 0.139)
+    constexpr int NPART = (NB == 4 && NW == 4) ? PMM_F32_DMA_PARTS_SMALL : PMM_F32_DMA_PARTS;
     static_assert(TP % NPART == 0 && NPART <= 4, "DMA pieces split evenly over the MFMA groups");
     __amdgpu_buffer_rsrc_t rb = rsrc_b(t0);
     stage(buf, rb, 0, t0, 0, TP);
