@@ -195,6 +195,76 @@ def numpy_comparator(q, c, k, reps=1, warm=0):
     return q.shape[0] / dt, dt
 
 
+def matmul_line(args, reps=20, warm=3):
+    """SURVEY 8f row 1, `.pmm.matmul` (matmul.rs:295-417): the f32 GEMM in store
+    mode through the host C ABI (pmm_matmul_f32: host Q, C in; the M x N f32
+    result in a host buffer), at the reference benchmark's size (configs[0]
+    inputs, seed 42).  Per call: median wall time of `reps` calls, the device
+    GEMM's average (HIP events) and the result's relative error against a
+    float64 product; CPU baseline: NumPy's f32 BLAS product (the role of the
+    reference's faer GEMM, matmul.rs:244-251)."""
+    from polars_matmul import _native
+
+    M, N, D = CONFIGS["c1"][:3]
+    qh, ch = ref_inputs(M, N, D)
+    out = _native.matmul_host(qh, ch)
+    ref = qh.astype(np.float64) @ ch.astype(np.float64).T
+    err = float(np.max(np.abs(out.astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref))))
+    del ref, out
+    for _ in range(warm):
+        _native.matmul_host(qh, ch)
+    _native.timing_reset()
+    _native.timing_enable(True)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _native.matmul_host(qh, ch)
+        ts.append(time.perf_counter() - t0)
+    # the same call into a reused (already faulted-in) output buffer: a fresh
+    # 40 MB result costs its page faults (~3 ms on the GPU box's host), which
+    # NumPy's product pays too
+    import ctypes
+
+    reuse = np.zeros((M, N), np.float32)
+    vp = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    rts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        _native.check(_native._lib.pmm_matmul_f32(vp(qh), M, vp(ch), N, D, vp(reuse)))
+        rts.append(time.perf_counter() - t0)
+    _native.timing_enable(False)
+    kms, kn = _native.timing_read("gemm_f32_matmul")
+    dt = float(np.median(ts))
+    rdt = float(np.median(rts))
+    flops = 2.0 * M * N * D
+    line = {
+        "metric": f"matmul calls/s ({M}x{N}x{D} f32, host buffers in and out)", "value": round(1.0 / dt, 2),
+        "unit": "calls/s", "ms_per_call": round(dt * 1000.0, 3),
+        "kernel_ms_avg": round(kms / kn, 4) if kn else None,
+        "kernel_tflops": round(flops / (kms / kn / 1000.0) / 1e12, 2) if kn else None,
+        "ms_per_call_reused_out": round(rdt * 1000.0, 3),
+        "out_gbs": round(M * N * 4 / dt / 1e9, 2), "max_rel_err_vs_f64": err,
+        "note": "result bytes M*N*4 = 40 MB per call: the host side (a fresh buffer's page faults, then "
+                "the PCIe copies), not the GEMM, bounds the call",
+    }
+    if args.cpu_sample:
+        for _ in range(2):
+            qh @ ch.T
+        cts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            qh @ ch.T
+            cts.append(time.perf_counter() - t0)
+        cdt = float(np.median(cts))
+        line["cpu_baseline"] = {
+            "value": round(1.0 / cdt, 2), "unit": "calls/s",
+            "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+            "host_nproc": os.cpu_count(), "kind": "port",
+            "sample": f"the full product, NumPy f32 BLAS q @ c.T, median of 5 after 2 warm-ups: {cdt * 1000:.2f} ms",
+        }
+    return line
+
+
 def boundary_rates(q_dev, c_dev, k, metric_id, compute=0):
     """Host-boundary rates: host f32 buffers in, host idx/score
     out, through the C ABI, one call each (untimed by the contract's clock):
@@ -503,8 +573,9 @@ def main():
                     help="queries timed on the CPU baseline vs the full corpus (0 = skip CPU baselines)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
-    ap.add_argument("--extra", default="c4,c1,c2",
-                    help="comma-separated secondary configs measured after the main line (N=1; 'none' = none)")
+    ap.add_argument("--extra", default="c4,c1,c2,matmul",
+                    help="comma-separated secondary configs measured after the main line (N=1; 'none' = none; "
+                         "'matmul' = .pmm.matmul at the c1 size)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 top-k")
     ap.add_argument("--cpu-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
@@ -579,7 +650,8 @@ def main():
         torch.cuda.empty_cache()
         extra = {}
         for name in [x for x in args.extra.split(",") if x and x not in (args.config, "none")]:
-            extra[name] = extra_line(name, args.steps, args.warmup, dev, args)
+            extra[name] = extra_line(name, args.steps, args.warmup, dev, args) if name != "matmul" \
+                else matmul_line(args)
             log(f"extra {name}: {json.dumps(extra[name])}")
 
     if rank != 0:
