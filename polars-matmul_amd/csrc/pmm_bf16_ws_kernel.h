@@ -85,6 +85,9 @@ constexpr int QCAP = 256;                    // survivor queue per epilogue wave
 // instead of 4 changed nothing, so the stream is bound by bandwidth, not by
 // the bytes in flight.)  The selection-based compaction (capg <=
 // kBf16WsMaxCapg) needs no LDS scratch, which leaves room for the 7th slot.
+#ifndef PMM_WS_EPI_OFFSET
+#define PMM_WS_EPI_OFFSET 1  // (A/B: 0 = epilogue groups from the tile's first interval)
+#endif
 #ifndef PMM_WS_NST
 #define PMM_WS_NST 7  // (diagnostic override: -DPMM_WS_NST=n)
 #endif
@@ -564,19 +567,24 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             tt = t2;
           }
           if (tile > t0 && a.ablate != 1 && a.ablate != 3) {
-            // column group c in interval ES * c, the drain in interval dks
-            // (all of tile - 1's hand-off reads done before interval KS - 1);
-            // every other interval when there are enough (KS >= 5): the DMA-
-            // only intervals between let the MFMA waves catch up (+0.6% at c4;
-            // PMM_ABLATE bit 6 = consecutive intervals)
+            // column group c in interval ES * c + EO, the drain in interval
+            // dks (all of tile - 1's hand-off reads done before interval KS -
+            // 1, where the MFMA waves rewrite the hand-off); every other
+            // interval when there are enough (KS >= 5): the DMA-only intervals
+            // between let the MFMA waves catch up (+0.6% at c4; PMM_ABLATE bit
+            // 6 = consecutive intervals), starting one interval into the tile
+            // (the MFMA waves' hand-off writes and the tile's first fragment
+            // reads go first: c4 147.1-147.3 vs 148.5-149.0 ms; groups three
+            // intervals apart 148.2)
             const bool str2 = KS >= 2 * NB + 1 && !(a.ablate & 64);
             const int ES = str2 ? 2 : 1;
-            const int dks = KS == 1 ? 0 : (str2 ? 2 * NB : NB - 1);
+            const int EO = str2 ? PMM_WS_EPI_OFFSET : 0;
+            const int dks = KS == 1 ? 0 : (str2 ? (EO ? KS - 1 : 2 * NB) : NB - 1);
             if (KS == 1) {
 #pragma unroll
               for (int c = 0; c < NB; c++) epilogue(tile - 1, c);
-            } else if (ks % ES == 0 && ks / ES < NB) {
-              epilogue(tile - 1, ks / ES);
+            } else if (ks >= EO && (ks - EO) % ES == 0 && (ks - EO) / ES < NB) {
+              epilogue(tile - 1, (ks - EO) / ES);
             }
             if (ks == dks && ((tile - t0) & 3) == 0 && qlen > 0) {
               wait_lgkm0();
