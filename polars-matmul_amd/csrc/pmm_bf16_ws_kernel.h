@@ -88,6 +88,10 @@ constexpr int QCAP = 256;                    // survivor queue per epilogue wave
 #ifndef PMM_WS_EPI_OFFSET
 #define PMM_WS_EPI_OFFSET 1  // (A/B: 0 = epilogue groups from the tile's first interval)
 #endif
+#ifndef PMM_WS_DRAIN_TILES
+#define PMM_WS_DRAIN_TILES 4  // (a queued survivor's column norm must stay in the 8-tile ring: <= 6)
+#endif
+static_assert(PMM_WS_DRAIN_TILES >= 1 && PMM_WS_DRAIN_TILES <= 6, "survivor drain period");
 #ifndef PMM_WS_NST
 #define PMM_WS_NST 7  // (diagnostic override: -DPMM_WS_NST=n)
 #endif
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             } else if (ks >= EO && (ks - EO) % ES == 0 && (ks - EO) / ES < NB) {
               epilogue(tile - 1, (ks - EO) / ES);
             }
-            if (ks == dks && ((tile - t0) & 3) == 0 && qlen > 0) {
+            if (ks == dks && ((tile - t0) % PMM_WS_DRAIN_TILES) == 0 && qlen > 0) {
               wait_lgkm0();
               drain();
             }
