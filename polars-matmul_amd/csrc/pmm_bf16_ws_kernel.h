@@ -73,7 +73,10 @@ constexpr int OFF_UNIT = OFF_LO + BM * 4;
 constexpr int OFF_CVR = (OFF_UNIT + 16 + 255) & ~255;   // pre-filter factors [CVT][BN]
 constexpr int OFF_CNR = OFF_CVR + CVT * BN * 4;          // column norms [CVT][BN]
 constexpr int OFF_HAND = (OFF_CNR + CVT * BN * 4 + 255) & ~255;  // [NHB][NWM][HAND]
-constexpr int QCAP = 256;                    // survivor queue per epilogue wave
+#ifndef PMM_WS_QCAP
+#define PMM_WS_QCAP 256
+#endif
+constexpr int QCAP = PMM_WS_QCAP;            // survivor queue per epilogue wave
 // The rest of the carve depends on the K-steps per tile.  With KS >= 3 the
 // epilogue waves are done with tile t's accumulators (read in the first two
 // intervals of tile t + 1) before the MFMA waves write tile t + 1's (after
@@ -100,9 +103,14 @@ struct Carve {
   static constexpr int NHB = KS >= 3 ? 1 : 2;              // hand-off buffers
   static constexpr int NST = KS >= 3 ? PMM_WS_NST : 5;     // corpus ring slots
   static constexpr int OFF_RING = OFF_HAND + NHB * NWM * HAND;
-  static constexpr int OFF_QUEUE = OFF_RING + NST * STAGE;  // [NWE][QCAP] u64
-  static constexpr int BYTES = OFF_QUEUE + NWE * QCAP * 8;
+  static constexpr int QC = KS >= 3 ? QCAP : 256;          // survivor queue entries per wave
+  static constexpr int OFF_QUEUE = OFF_RING + NST * STAGE;  // [NWE][QC] u64
+  static constexpr int BYTES = OFF_QUEUE + NWE * QC * 8;
   static_assert(BYTES <= 160 * 1024, "LDS carve");
+  // (diagnostic overrides: 5 slots passed the bf16 tests at 156 ms; 6 slots
+  // at KS = 6 -- ring slot == K step -- returned wrong scores and ran 2.6x
+  // slower, a failure not understood yet; 7, the default, is never equal to KS)
+  static_assert(KS < 3 || NST != KS, "PMM_WS_NST equal to the K steps per tile measured incorrect");
   static_assert(OFF_RING % 256 == 0 && STAGE % 1024 == 0, "LDS carve alignment");
 };
 static_assert(P * NWE * 1024 == STAGE, "a K-step splits into whole 1 KiB pieces per wave");
@@ -432,6 +440,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       // every 4 tiles (the column-norm ring holds the last 8) and at the
       // unit's end.  Queue writes are asm: hipcc would wait for the in-flight
       // ring DMAs before every LDS store it sees.
+      constexpr int QCAP = C::QC;
       const uint32_t lq_lds = (uint32_t)(size_t)(LDS_AS char *)(smem + C::OFF_QUEUE) + rw * QCAP * 8;
       const u64 *lq = (const u64 *)(smem + C::OFF_QUEUE) + rw * QCAP;
       int qlen = 0;  // wave-uniform
