@@ -88,8 +88,14 @@ constexpr int QCAP = PMM_WS_QCAP;            // survivor queue per epilogue wave
 // instead of 4 changed nothing, so the stream is bound by bandwidth, not by
 // the bytes in flight.)  The selection-based compaction (capg <=
 // kBf16WsMaxCapg) needs no LDS scratch, which leaves room for the 7th slot.
+#ifndef PMM_WS_EPI_SPACING
+#define PMM_WS_EPI_SPACING 2  // (A/B: intervals between the epilogue's column groups, KS >= 6)
+#endif
+#ifndef PMM_WS_DRAIN_INTERVAL
+#define PMM_WS_DRAIN_INTERVAL -1  // (A/B: interval of the periodic drain; -1 = the schedule's)
+#endif
 #ifndef PMM_WS_EPI_OFFSET
-#define PMM_WS_EPI_OFFSET 1  // (A/B: 0 = epilogue groups from the tile's first interval)
+#define PMM_WS_EPI_OFFSET -1  // (A/B: -1 = by K steps (2 at KS >= 6, else 1); 0 = from the first interval)
 #endif
 #ifndef PMM_WS_DRAIN_TILES
 #define PMM_WS_DRAIN_TILES 4  // (a queued survivor's column norm must stay in the 8-tile ring: <= 6)
@@ -585,14 +591,22 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             // 1, where the MFMA waves rewrite the hand-off); every other
             // interval when there are enough (KS >= 5): the DMA-only intervals
             // between let the MFMA waves catch up (+0.6% at c4; PMM_ABLATE bit
-            // 6 = consecutive intervals), starting one interval into the tile
-            // (the MFMA waves' hand-off writes and the tile's first fragment
-            // reads go first: c4 147.1-147.3 vs 148.5-149.0 ms; groups three
-            // intervals apart 148.2)
-            const bool str2 = KS >= 2 * NB + 1 && !(a.ablate & 64);
-            const int ES = str2 ? 2 : 1;
-            const int EO = str2 ? PMM_WS_EPI_OFFSET : 0;
-            const int dks = KS == 1 ? 0 : (str2 ? (EO ? KS - 1 : 2 * NB) : NB - 1);
+            // 6 = consecutive intervals), starting one or two intervals into
+            // the tile (the MFMA waves' hand-off writes and the tile's first
+            // fragment reads go first: c4 147.1-147.3 vs 148.5-149.0 ms for one;
+            // groups three intervals apart 148.2; drain in interval 0 worse)
+            constexpr bool STR2 = KS >= 2 * NB + 1;
+            constexpr int ES2 = KS >= 6 ? PMM_WS_EPI_SPACING : 2;
+            // (offset 2 where the K steps allow: c4 151.1-151.4 vs 151.6-151.9
+            // ms with offset 1, alternated)
+            constexpr int EO2 = PMM_WS_EPI_OFFSET >= 0 ? PMM_WS_EPI_OFFSET : (KS >= 6 ? 2 : 1);
+            // every group's hand-off reads end before interval KS - 1
+            static_assert(!STR2 || EO2 + ES2 * (NB - 1) <= KS - 2, "epilogue schedule overlaps the hand-off");
+            const bool str2 = STR2 && !(a.ablate & 64);
+            const int ES = str2 ? ES2 : 1;
+            const int EO = str2 ? EO2 : 0;
+            const int dks = KS == 1 ? 0 : (str2 ? (PMM_WS_DRAIN_INTERVAL >= 0 ? PMM_WS_DRAIN_INTERVAL % KS
+                                                   : (EO ? KS - 1 : 2 * NB)) : NB - 1);
             if (KS == 1) {
 #pragma unroll
               for (int c = 0; c < NB; c++) epilogue(tile - 1, c);
