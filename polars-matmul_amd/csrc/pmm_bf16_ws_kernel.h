@@ -102,7 +102,7 @@ constexpr int QCAP = PMM_WS_QCAP;            // survivor queue per epilogue wave
 #endif
 static_assert(PMM_WS_DRAIN_TILES >= 1 && PMM_WS_DRAIN_TILES <= 6, "survivor drain period");
 #ifndef PMM_WS_NST
-#define PMM_WS_NST 7  // (diagnostic override: -DPMM_WS_NST=n)
+#define PMM_WS_NST 7  // (A/B override: -DPMM_WS_NST=n)
 #endif
 template <int KS>
 struct Carve {
@@ -113,10 +113,15 @@ struct Carve {
   static constexpr int OFF_QUEUE = OFF_RING + NST * STAGE;  // [NWE][QC] u64
   static constexpr int BYTES = OFF_QUEUE + NWE * QC * 8;
   static_assert(BYTES <= 160 * 1024, "LDS carve");
-  // (diagnostic overrides: 5 slots passed the bf16 tests at 156 ms; 6 slots
-  // at KS = 6 -- ring slot == K step -- returned wrong scores and ran 2.6x
-  // slower, a failure not understood yet; 7, the default, is never equal to KS)
-  static_assert(KS < 3 || NST != KS, "PMM_WS_NST equal to the K steps per tile measured incorrect");
+  // When NST divides KS the slot sequence repeats every tile, so the slot at
+  // a tile's start is loop-invariant; left visible, hipcc hoisted every
+  // K-step's ring addresses out of the tile loop, ran out of VGPRs and
+  // spilled inside the MFMA loop (592 B per lane at NST = KS = 6).  Its spill
+  // and reload code is not padded for the inline-asm MFMAs it cannot see
+  // (stale accumulators and fragments: wrong scores, 2.6x slower).  The
+  // kernel makes the slot opaque per tile in that case (SLOT_REPEATS);
+  // tests/test_kernel_resources.py keeps spill code out of the MFMA loops.
+  static constexpr bool SLOT_REPEATS = KS % NST == 0;
   static_assert(OFF_RING % 256 == 0 && STAGE % 1024 == 0, "LDS carve alignment");
 };
 static_assert(P * NWE * 1024 == STAGE, "a K-step splits into whole 1 KiB pieces per wave");
@@ -309,6 +314,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       const uint32_t ring_lds = (uint32_t)(size_t)(LDS_AS char *)ring;
       int sl = 0;
       for (int tile = t0; tile < t1; tile++) {
+        if constexpr (C::SLOT_REPEATS) asm volatile("" : "+s"(sl));  // (see Carve)
         f32x16 acc[NB];
         bf16x8 bq[PF + 1][NB];  // fragment sets: PF in flight + the one in use
 #pragma unroll
@@ -561,6 +567,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       }
       int sl = 0;
       for (int tile = t0; tile < t1; tile++) {
+        if constexpr (C::SLOT_REPEATS) asm volatile("" : "+s"(sl));  // (see Carve)
         // unrolled: compile-time slot / count arithmetic (a runtime K-step
         // loop, 40% less code, measured 12% slower at c4: the epilogue waves'
         // per-interval instructions are on the critical path)

@@ -1,0 +1,101 @@
+"""Build-level guard for the inline-asm MFMA kernels (CPU only: hipcc
+cross-compiles gfx950 here; skipped where hipcc is absent).
+
+The bf16 kernels issue their MFMAs from inline asm, so LLVM cannot see them
+and pads none of their register hazards.  Any spill or reload the register
+allocator puts next to them is unpadded: at PMM_WS_NST = KS = 6 the
+wave-specialised kernel spilled 592 B per lane into its MFMA loop and
+returned wrong scores (csrc/pmm_bf16_ws_kernel.h, Carve::SLOT_REPEATS).  This
+test compiles every instantiation to ISA and asserts that no basic block
+holding an MFMA holds scratch (spill) code.
+"""
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "polars-matmul_amd", "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+         "--cuda-device-only", "-S"]
+
+# (source, defines): every padded-D instantiation of the wave-specialised
+# kernel, the ring sizes whose slot sequence repeats per tile, and the
+# other two bf16 kernels at the largest D
+BUILDS = [("pmm_bf16_ws_ks.hip", [f"-DPMM_BF16_KS={k}"]) for k in range(1, 7)] + [
+    ("pmm_bf16_ws_ks.hip", ["-DPMM_BF16_KS=6", "-DPMM_WS_NST=6"]),
+    ("pmm_bf16_ws_ks.hip", ["-DPMM_BF16_KS=6", "-DPMM_WS_NST=3"]),
+    ("pmm_bf16_ks.hip", ["-DPMM_BF16_KS=6"]),
+    ("pmm_bf16_wide_ks.hip", ["-DPMM_BF16_KS=6"]),
+]
+
+_LABEL = re.compile(r"^(\.LBB\S*:|; %bb\.\d+:)")
+
+
+def mfma_blocks_with_spills(asm: str):
+    """(function, block label) of every basic block with both an MFMA and a
+    scratch access."""
+    bad, func, label, has_mfma, has_scr = [], None, None, False, False
+
+    def close():
+        if has_mfma and has_scr:
+            bad.append((func, label))
+
+    for line in asm.splitlines():
+        if re.match(r"^_Z\S+:", line):
+            close()
+            func, label, has_mfma, has_scr = line.split(":")[0], "entry", False, False
+            continue
+        if _LABEL.match(line) or line.strip().startswith("s_endpgm"):
+            close()
+            label, has_mfma, has_scr = line.split(":")[0], False, False
+            continue
+        s = line.strip()
+        if s.startswith("v_mfma"):
+            has_mfma = True
+        elif s.startswith("scratch_"):
+            has_scr = True
+    close()
+    return bad
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+def test_no_spill_code_beside_inline_asm_mfmas():
+    tmp = tempfile.mkdtemp(prefix="pmm_isa_")
+    try:
+        procs = []
+        for i, (src, defs) in enumerate(BUILDS):
+            out = os.path.join(tmp, f"b{i}.s")
+            cmd = [HIPCC, *FLAGS, *defs, "-I", CSRC, "-o", out, os.path.join(CSRC, src)]
+            procs.append((src, defs, out, subprocess.Popen(cmd, stdout=subprocess.PIPE,
+                                                           stderr=subprocess.STDOUT)))
+        failures = []
+        for src, defs, out, p in procs:
+            log = p.communicate(timeout=600)[0].decode(errors="replace")
+            assert p.returncode == 0, f"{src} {defs}: {log[-2000:]}"
+            with open(out) as f:
+                asm = f.read()
+            assert "v_mfma" in asm, f"{src} {defs}: no MFMA in the ISA"
+            bad = mfma_blocks_with_spills(asm)
+            if bad:
+                failures.append(f"{src} {' '.join(defs)}: {bad[:4]}")
+        assert not failures, "spill code in MFMA blocks:\n" + "\n".join(failures)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def test_detector_flags_a_spill_in_an_mfma_block():
+    asm = "\n".join([
+        "_Zkern:",
+        ".LBB0_1:",
+        "\tv_mfma_f32_32x32x16_bf16 v[0:15], v[16:19], v[20:23], v[0:15]",
+        "\tscratch_load_dwordx4 v[16:19], off, off",
+        ".LBB0_2:",
+        "\tscratch_store_dword off, v3, off",
+        "\ts_endpgm",
+    ])
+    assert mfma_blocks_with_spills(asm) == [("_Zkern", ".LBB0_1")]
