@@ -66,6 +66,10 @@ int pmm_metric_from_str(const char *s, int *metric);
 int pmm_metric_higher_is_better(int metric);
 
 int pmm_device_count(int *count);
+/* Free and total HBM of the device this thread's host calls run on
+ * (hipMemGetInfo); the corpus cache sizes itself by it.  No reference
+ * counterpart (the reference has no device memory). */
+int pmm_device_memory(size_t *free_bytes, size_t *total_bytes);
 /* Selects the HIP device used by later calls on this thread. */
 int pmm_set_device(int device);
 

@@ -972,6 +972,15 @@ int pmm_device_count(int *count) {
   return PMM_OK;
 }
 
+int pmm_device_memory(size_t *free_bytes, size_t *total_bytes) {
+  if (!free_bytes || !total_bytes) return fail(PMM_ERR_ARG, "null argument");
+  int dev, rc;
+  DevScope scope;
+  if ((rc = ensure_device(&dev, &scope))) return rc;
+  HIP_TRY(hipMemGetInfo(free_bytes, total_bytes));
+  return PMM_OK;
+}
+
 int pmm_set_device(int device) {
   int n = 0;
   pmm_device_count(&n);

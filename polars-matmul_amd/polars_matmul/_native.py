@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "pmm_metric_from_str",
     "pmm_metric_higher_is_better",
     "pmm_device_count",
+    "pmm_device_memory",
     "pmm_set_device",
     "pmm_topk_f32",
     "pmm_topk_f32_ex",
@@ -109,6 +110,7 @@ _SIGS = {
     "pmm_metric_from_str": ([ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)], _i32),
     "pmm_metric_higher_is_better": ([_i32], _i32),
     "pmm_device_count": ([ctypes.POINTER(ctypes.c_int)], _i32),
+    "pmm_device_memory": ([ctypes.POINTER(_sz), ctypes.POINTER(_sz)], _i32),
     "pmm_set_device": ([_i32], _i32),
     "pmm_topk_f32": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_topk_f32_ex": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _i32, _vp, _vp], _i32),
@@ -182,6 +184,13 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     check(_lib.pmm_device_count(ctypes.byref(n)))
     return n.value
+
+
+def device_memory():
+    """(free, total) bytes of HBM on the device host calls run on."""
+    f, t = _sz(0), _sz(0)
+    check(_lib.pmm_device_memory(ctypes.byref(f), ctypes.byref(t)))
+    return f.value, t.value
 
 
 def metric_from_str(s: str) -> int:

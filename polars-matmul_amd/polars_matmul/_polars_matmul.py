@@ -184,7 +184,9 @@ def _as_usize(k) -> int:
 # meanwhile).  Arrow data is immutable by contract: a Series that shares
 # memory with a numpy array the caller then writes to in place gives stale
 # cached results -- clear_corpus_cache() or PMM_CORPUS_CACHE=0 in that case.
-# PMM_CORPUS_CACHE_BYTES bounds the HBM the cache holds (default 8 GiB).
+# PMM_CORPUS_CACHE_BYTES bounds the HBM the cache holds (default 8 GiB), and
+# a corpus is cached only while it takes at most half of the device's free HBM
+# (pmm_device_memory), so the cache never crowds out the searches themselves.
 # Handles are reference-counted (DeviceCorpus.acquire/release), so evicting
 # or clearing never frees a corpus another thread is searching.
 # ---------------------------------------------------------------------------
@@ -194,6 +196,14 @@ _cache: "collections.OrderedDict" = collections.OrderedDict()
 _CACHE_ON = os.environ.get("PMM_CORPUS_CACHE", "1") != "0"
 _CACHE_BYTES = int(os.environ.get("PMM_CORPUS_CACHE_BYTES", str(8 << 30)))
 _CACHE_MIN_BYTES = 1 << 20  # small corpora are cheaper to upload than to cache
+
+
+def _fits_device(nbytes: int) -> bool:
+    try:
+        free, _ = _native.device_memory()
+    except _native.PmmError:
+        return False
+    return nbytes <= free // 2
 
 
 def _arrow_key(arr):
@@ -217,6 +227,8 @@ def _cached_corpus(original, rv, c: np.ndarray):
         if hit is not None:
             _cache.move_to_end(key)
             return hit[1].acquire()
+        if not _fits_device(c.nbytes):
+            return None
         dc = _native.DeviceCorpus(c)
         _cache[key] = (rv, dc)
         total = sum(v[1].nbytes for v in _cache.values())

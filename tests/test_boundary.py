@@ -5,6 +5,7 @@ src/matmul.rs / src/lib.rs) behaves as the reference does before any device
 work is issued.  No compute calls without a GPU."""
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 import re
@@ -233,3 +234,36 @@ def test_device_corpus_refcount_defers_destroy(monkeypatch):
     assert destroyed == [1234] and dc.closed
     dc.close()
     assert destroyed == [1234]
+
+
+def test_corpus_cache_respects_free_device_memory(monkeypatch):
+    # the cache takes at most half of the free HBM -- a
+    # corpus larger than that is searched uncached, one that fits is cached
+    from polars_matmul import _polars_matmul as pm
+
+    created = []
+
+    class StubCorpus:
+        def __init__(self, c):
+            self.nbytes = c.nbytes
+            created.append(self)
+
+        def acquire(self):
+            return self
+
+        def close(self):
+            pass
+
+    free = {"bytes": 0}
+    monkeypatch.setattr(_native, "DeviceCorpus", StubCorpus)
+    monkeypatch.setattr(_native, "device_memory", lambda: (free["bytes"], 1 << 40))
+    monkeypatch.setattr(pm, "_CACHE_ON", True)
+    monkeypatch.setattr(pm, "_cache", collections.OrderedDict())
+    c = np.zeros((4096, 128), dtype=np.float32)  # 2 MiB: above the caching floor
+    arr = pa.FixedSizeListArray.from_arrays(pa.array(c.reshape(-1)), 128)
+    free["bytes"] = 3 << 20  # half of it (1.5 MiB) is below the corpus
+    assert pm._cached_corpus(arr, arr, c) is None and created == []
+    free["bytes"] = 8 << 20
+    dc = pm._cached_corpus(arr, arr, c)
+    assert dc is created[0] and len(pm._cache) == 1
+    assert pm._cached_corpus(arr, arr, c) is dc and len(created) == 1  # hit
