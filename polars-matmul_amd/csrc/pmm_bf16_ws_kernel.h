@@ -101,9 +101,6 @@ constexpr int QCAP = PMM_WS_QCAP;            // survivor queue per epilogue wave
 #define PMM_WS_DRAIN_TILES 4  // (a queued survivor's column norm must stay in the 8-tile ring: <= 6)
 #endif
 static_assert(PMM_WS_DRAIN_TILES >= 1 && PMM_WS_DRAIN_TILES <= 6, "survivor drain period");
-#ifndef PMM_WS_BITSASM
-#define PMM_WS_BITSASM 1  // (A/B: 0 = survivor bits by the compiler's compare/select/or sequence)
-#endif
 #ifndef PMM_WS_NST
 #define PMM_WS_NST 7  // (A/B override: -DPMM_WS_NST=n)
 #endif
@@ -529,24 +526,8 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
         if (__ballot(any) == 0ull || (a.ablate & 8)) return;  // (8: benchmarking, pre-filter only)
         const uint64_t tq0 = stamp();
         uint32_t bits = 0u;
-        if (PMM_WS_BITSASM) {
-          // bits = 2 * bits + !(d < 0) per score: v_cmp_ngt (true for NaN)
-          // into VCC, then add-with-carry (2 wait states between the VALU's
-          // VCC write and its read, which hipcc does not insert inside asm)
 #pragma unroll
-          for (int q = 0; q < 4; q++)
-            asm volatile(
-                "v_cmp_ngt_f32 vcc, 0, %1\n\ts_nop 1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-                "v_cmp_ngt_f32 vcc, 0, %2\n\ts_nop 1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-                "v_cmp_ngt_f32 vcc, 0, %3\n\ts_nop 1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc\n\t"
-                "v_cmp_ngt_f32 vcc, 0, %4\n\ts_nop 1\n\tv_addc_co_u32 %0, vcc, %0, %0, vcc"
-                : "+v"(bits)
-                : "v"(d[4 * q]), "v"(d[4 * q + 1]), "v"(d[4 * q + 2]), "v"(d[4 * q + 3])
-                : "vcc");
-        } else {
-#pragma unroll
-          for (int e = 0; e < 16; e++) bits = (bits << 1) | (uint32_t)!(d[e] < 0.0f);
-        }
+        for (int e = 0; e < 16; e++) bits = (bits << 1) | (uint32_t)!(d[e] < 0.0f);
         if (!any) bits = 0u;
         const float *hf = (const float *)(hb + ((c * 4) * 64 + lane) * 16);
         for (;;) {

@@ -29,7 +29,6 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
 BUILDS = [("pmm_bf16_ws_ks.hip", [f"-DPMM_BF16_KS={k}"]) for k in range(1, 7)] + [
     ("pmm_bf16_ws_ks.hip", ["-DPMM_BF16_KS=6", "-DPMM_WS_NST=6"]),
     ("pmm_bf16_ws_ks.hip", ["-DPMM_BF16_KS=6", "-DPMM_WS_NST=3"]),
-    ("pmm_bf16_ws_ks.hip", ["-DPMM_BF16_KS=6", "-DPMM_WS_BITSASM=0"]),
     ("pmm_bf16_ks.hip", ["-DPMM_BF16_KS=6"]),
     ("pmm_bf16_wide_ks.hip", ["-DPMM_BF16_KS=6"]),
 ]
