@@ -3,7 +3,7 @@
 # the SQC instruction-cache counters the box offers, then one PMC pass with them
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/icache
+O=$R/gpurun_out/icache${ICACHE_TAG:-}
 mkdir -p "$O"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 -L > "$O/counters.txt" 2>&1 || exit 1
