@@ -66,6 +66,30 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def available_parallelism() -> int:
+    """The thread count faer's Parallelism::Rayon(0) gets (metrics.rs:244-251):
+    rayon's default pool is std::thread::available_parallelism(), i.e. the
+    CPUs this process may run on (sched_getaffinity), capped by a cgroup v2
+    CPU quota (cpu.max) when one is set."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def recall_at_k(a: np.ndarray, b: np.ndarray) -> float:
+    """Mean over rows of |a_row & b_row| / k for index lists without
+    duplicates inside a row (SURVEY 8c's bf16 criterion)."""
+    both = np.concatenate([a, b], axis=1)
+    both.sort(axis=1)
+    return float(np.mean((both[:, 1:] == both[:, :-1]).sum(axis=1) / a.shape[1]))
+
+
 # ---------------------------------------------------------------------------
 # N-rank launcher (no GPU work in this process)
 # ---------------------------------------------------------------------------
@@ -259,7 +283,7 @@ def matmul_line(args, reps=20, warm=3):
         line["cpu_baseline"] = {
             "value": round(1.0 / cdt, 2), "unit": "calls/s",
             "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-            "host_nproc": os.cpu_count(), "kind": "port",
+            "host_nproc": os.cpu_count(), "available_parallelism": available_parallelism(), "kind": "port",
             "sample": f"the full product, NumPy f32 BLAS q @ c.T, median of 5 after 2 warm-ups: {cdt * 1000:.2f} ms",
         }
     return line
@@ -476,6 +500,7 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8):
             savg = ks["shard_merge"][0] / 1000.0
             reduction["shard_merge"] = {"bytes_per_launch": sbytes, "kernel_ms_avg": round(savg * 1000.0, 3),
                                         "achieved": round(sbytes / savg / 1e9, 1), "unit": "GB/s"}
+    lists = out_i.cpu().numpy() if (world == 1 or rank == 0) else None
     fields = {
         "config": {"workload": f"{M}x{N}x{D} {cdt} {metric} k={k} ({name})", "queries": M, "corpus": N,
                    "dim": D, "k": k, "metric": metric,
@@ -485,7 +510,7 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8):
         "roofline": roof, "reduction_roofline": reduction, "check": check,
     }
     del runner, ws
-    return fields, q, c
+    return fields, q, c, lists
 
 
 def cpu_selftest(args, rank, world):
@@ -537,14 +562,20 @@ def extra_line(name, steps, warmup, dev, args):
     M, N, D = CONFIGS[name][:3]
     small = M * N * D < 10**11  # sub-millisecond steps: time more of them
     st, wu = (max(steps, 200), max(warmup, 10)) if small else (steps, warmup)
-    fields, q, c = measure(name, st, wu, 0, 1, None, dev, check_rows=8)
+    fields, q, c, lists = measure(name, st, wu, 0, 1, None, dev, check_rows=8)
+    ref = args.ref_lists.get(CONFIGS[name][:5])
+    if CONFIGS[name][5] == "bf16" and ref is not None and fields["check"] is not None:
+        # SURVEY 8c's bf16 bar: recall@k of the bf16 lists against the f32
+        # lists of the same rows (the main line's c3 output, same inputs)
+        fields["check"]["recall_at_k_vs_f32_all_rows"] = round(recall_at_k(lists, ref), 6)
+    del lists
     if name in REF_INPUT_CONFIGS and args.cpu_sample:
         k, metric = CONFIGS[name][3], CONFIGS[name][4]
         qh, ch = ref_inputs(M, N, D)
         qps, dt = cpu_oracle_qps(qh, ch, k, metric, args.cpu_threads, reps=5, warm=2)
         fields["cpu_baseline"] = {
             "value": round(qps, 2), "unit": "queries/s", "cores": args.cpu_threads,
-            "host_nproc": os.cpu_count(), "kind": "port",
+            "host_nproc": os.cpu_count(), "available_parallelism": available_parallelism(), "kind": "port",
             "sample": f"the full {M}x{N}x{D} {metric} k={k} workload (seed-42 inputs, "
                       f"benchmark_topk.py:69-71), median of 5 after 2 warm-ups: {dt * 1000:.1f} ms; "
                       "oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select)",
@@ -554,7 +585,7 @@ def extra_line(name, steps, warmup, dev, args):
             fields["cpu_baseline_numpy"] = {
                 "value": round(nq, 2), "unit": "queries/s",
                 "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-                "host_nproc": os.cpu_count(), "kind": "port",
+                "host_nproc": os.cpu_count(), "available_parallelism": available_parallelism(), "kind": "port",
                 "sample": f"full workload, median of 5 after 2 warm-ups: {ndt * 1000:.1f} ms; the reference "
                           "README's NumPy comparator (benchmark_topk.py:14-33)",
             }
@@ -571,7 +602,8 @@ def main():
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--cpu-sample", type=int, default=512,
                     help="queries timed on the CPU baseline vs the full corpus (0 = skip CPU baselines)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="oracle baseline threads (0 = available_parallelism(), as faer's Rayon(0))")
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
     ap.add_argument("--extra", default="c4,c1,c2,matmul",
                     help="comma-separated secondary configs measured after the main line (N=1; 'none' = none; "
@@ -592,6 +624,8 @@ def main():
     if args.cpu_selftest:
         cpu_selftest(args, rank, world)
         return
+    if args.cpu_threads <= 0:
+        args.cpu_threads = available_parallelism()
 
     import torch
 
@@ -610,9 +644,12 @@ def main():
     _native.check(_native.lib().pmm_set_device(torch.cuda.current_device()))
 
     M, N, D, k, metric, cdt = CONFIGS[args.config]
-    fields, q, c = measure(args.config, args.steps, args.warmup, rank, world, dist, dev, args.check)
+    fields, q, c, lists = measure(args.config, args.steps, args.warmup, rank, world, dist, dev, args.check)
     if fields["check"]:
         log(f"spot check: {fields['check']}")
+    # f32 lists of this workload's (M, N, D, k, metric) for the bf16 recall check of an extra line
+    args.ref_lists = {CONFIGS[args.config][:5]: lists} if cdt == "f32" and lists is not None else {}
+    del lists
 
     boundary = None
     if args.boundary and world == 1 and args.config not in ("c5",):
@@ -629,7 +666,7 @@ def main():
         cpu_qps, cpu_dt = cpu_oracle_qps(qh, ch, k, metric, args.cpu_threads)
         cpu = {
             "value": round(cpu_qps, 2), "unit": "queries/s", "cores": args.cpu_threads,
-            "host_nproc": os.cpu_count(), "kind": "port",
+            "host_nproc": os.cpu_count(), "available_parallelism": available_parallelism(), "kind": "port",
             "sample": f"first {n_s} queries x full {N}-row corpus, {D}d {cdt} {metric} k={k}; "
                       f"oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select), {cpu_dt:.1f}s",
         }
@@ -638,7 +675,7 @@ def main():
             cpu_np = {
                 "value": round(np_qps, 2), "unit": "queries/s",
                 "cores": int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-                "host_nproc": os.cpu_count(), "kind": "port",
+                "host_nproc": os.cpu_count(), "available_parallelism": available_parallelism(), "kind": "port",
                 "sample": f"first {n_s} queries x full {N}-row corpus; the reference README's NumPy "
                           f"comparator (normalise, BLAS GEMM, argpartition, argsort), {np_dt:.1f}s",
             }

@@ -70,8 +70,27 @@ int pmm_device_count(int *count);
  * (hipMemGetInfo); the corpus cache sizes itself by it.  No reference
  * counterpart (the reference has no device memory). */
 int pmm_device_memory(size_t *free_bytes, size_t *total_bytes);
-/* Selects the HIP device used by later calls on this thread. */
+/* Selects the HIP device that later HOST-buffer calls on this thread run on
+ * (pmm_topk_f32*, pmm_topk_f64, pmm_matmul_*, pmm_corpus_create_f32,
+ * pmm_device_memory); they restore the caller's current device on return.
+ * Device-pointer entry points (*_device) ignore it and run on the caller's
+ * current HIP device (hipSetDevice), where their pointers live. */
 int pmm_set_device(int device);
+
+/* Multi-GPU through the drop-in boundary (no reference
+ * counterpart -- the reference is single-process, src/lib.rs:33-55).  With a
+ * list of n >= 2 devices, pmm_topk_f32 / pmm_topk_f32_ex (k <= 1024) and
+ * corpora created afterwards by pmm_corpus_create_f32 row-shard the corpus
+ * over the list, one contiguous shard per entry (sizes differ by <= 1; at most
+ * n shards).  Every device runs the fused top-k on its shard with global
+ * indices, the per-shard [2][m][k] lists are copied peer to peer (xGMI) to
+ * ids[0] and k-way merged there: the result equals the one-device result bit
+ * for bit.  A device may be listed more than once (one shard per entry).
+ * Process-wide; n = 0 (or ids = NULL) returns to one device.  f64, k > 1024
+ * and pmm_matmul_* stay on one device (pmm_set_device's). */
+int pmm_set_devices(const int *ids, int n);
+/* The current device list: *n entries, the first min(cap, *n) copied to ids. */
+int pmm_get_devices(int *ids, int cap, int *n);
 
 /* ---------------------------------------------------------------------------
  * Host-buffer entry points (what `_topk` / `_matmul` call; src/lib.rs:15-55).
@@ -190,13 +209,17 @@ int pmm_merge_topk_strided_device(const uint32_t *idx, const float *score, int64
  * corpus Series: python/polars_matmul/__init__.py:115-119).  The handle keeps
  * the padded rows in HBM and the norms of every metric (src/metrics.rs:368-393,
  * computed once at creation).  A handle may be used from several threads
- * concurrently; it is bound to the device current at creation.
+ * concurrently; it is bound to the device current at creation, or sharded over
+ * the device list (pmm_set_devices) in effect then.
  * ------------------------------------------------------------------------- */
 typedef struct pmm_corpus pmm_corpus;
 
 int pmm_corpus_create_f32(const float *c, int64_t n, int64_t d, pmm_corpus **out);
 int pmm_corpus_destroy(pmm_corpus *corpus);
 int pmm_corpus_info(const pmm_corpus *corpus, int64_t *n, int64_t *d, int *device);
+/* Number of device shards of a corpus handle (1, or the device list's length
+ * capped at n when pmm_set_devices was in effect at creation). */
+int pmm_corpus_shards(const pmm_corpus *corpus, int *shards);
 
 /* pmm_topk_f32 against a device-resident corpus (host queries in, host
  * results out; 0 <= k <= n). */

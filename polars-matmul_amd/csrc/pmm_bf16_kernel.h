@@ -306,7 +306,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
     int qlen = 0;  // this wave's queued items (wave-uniform)
     auto drain = [&]() {
       st_q += (uint32_t)qlen;
-      if (a.ablate == 2 || qlen == 0) {
+      if (PMM_ABL(a.ablate) == 2 || qlen == 0) {
         qlen = 0;
         return;
       }
@@ -371,7 +371,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
           const bool act = b != 0u;
           const u64 m = __ballot(act);
           if (m == 0ull) break;
-          if (act && a.ablate != 2) {
+          if (act && PMM_ABL(a.ablate) != 2) {
             const int j = 31 - __builtin_clz(b);  // bit j <-> row e = 15 - j
             b &= ~(1u << j);
             const int e = 15 - j;
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
       mfma_drain(acc);
       const uint64_t tte = timing ? __builtin_amdgcn_s_memtime() : 0;
       if (timing) cy_loop += tte - tts;
-      if (PIPE && has_prev && a.ablate != 1) extract(pv, pt, bits);
+      if (PIPE && has_prev && PMM_ABL(a.ablate) != 1) extract(pv, pt, bits);
       if (timing) cy_ext += __builtin_amdgcn_s_memtime() - tte;
     };
 
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
         tile_step(accA, accB, tile, tile > t0);
         if (tile + 1 < t1) tile_step(accB, accA, tile + 1, true);
       }
-      if (a.ablate != 1) {
+      if (PMM_ABL(a.ablate) != 1) {
         if (((t1 - 1 - t0) & 1) == 0) tile_last(accA, t1 - 1);
         else tile_last(accB, t1 - 1);
       }
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
       f32x16 acc[NB];
       for (int tile = t0; tile < t1; tile++) {
         tile_step(acc, acc, tile, false);
-        if (a.ablate != 1) {
+        if (PMM_ABL(a.ablate) != 1) {
           const uint64_t tx = timing ? __builtin_amdgcn_s_memtime() : 0;
           tile_last(acc, tile);
           if (timing) cy_ext += __builtin_amdgcn_s_memtime() - tx;

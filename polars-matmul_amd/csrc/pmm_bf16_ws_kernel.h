@@ -422,7 +422,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       // one K-step's DMA: corpus pieces into ring slot `slot`, plus on a
       // tile's first step this wave's share of its column factors / norms
       auto stage = [&](int slot, int tile, int ks) __attribute__((always_inline)) {
-        if (a.ablate == 3) return;  // benchmarking only: no corpus traffic at all
+        if (PMM_ABL(a.ablate) == 3) return;  // benchmarking only: no corpus traffic at all
         const int col0 = tile * BN;
         const __amdgpu_buffer_rsrc_t rb =
             make_rsrc(a.cb + (int64_t)col0 * a.ldc, (int64_t)max(0, min(BN, a.N - col0)) * a.ldc * 2);
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
         for (int q = 0; q < 4; q++) v4[q] = *(const f32x4 *)(hb + ((c * 4 + q) * 64 + lane) * 16);
         const int tc = 32 * c + r32;
         const int gcol = pt * BN + tc;
-        if (a.ablate & 32) {  // benchmarking only: the hand-off reads, nothing else
+        if (PMM_ABL(a.ablate) & 32) {  // benchmarking only: the hand-off reads, nothing else
           asm volatile("" ::"v"(v4[0]), "v"(v4[1]), "v"(v4[2]), "v"(v4[3]));
           return;
         }
@@ -523,7 +523,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
 #pragma unroll
         for (int e = 1; e < 16; e++) dm = __builtin_elementwise_maximum(dm, d[e]);
         const bool any = !(dm < 0.0f) && gcol < a.N;
-        if (__ballot(any) == 0ull || (a.ablate & 8)) return;  // (8: benchmarking, pre-filter only)
+        if (__ballot(any) == 0ull || (PMM_ABL(a.ablate) & 8)) return;  // (8: benchmarking, pre-filter only)
         const uint64_t tq0 = stamp();
         uint32_t bits = 0u;
 #pragma unroll
@@ -592,7 +592,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             cy0 += t2 - tt;
             tt = t2;
           }
-          if (tile > t0 && a.ablate != 1 && a.ablate != 3) {
+          if (tile > t0 && PMM_ABL(a.ablate) != 1 && PMM_ABL(a.ablate) != 3) {
             // column group c in interval ES * c + EO, the drain in interval
             // dks (all of tile - 1's hand-off reads done before interval KS -
             // 1, where the MFMA waves rewrite the hand-off); every other
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             constexpr int EO2 = PMM_WS_EPI_OFFSET >= 0 ? PMM_WS_EPI_OFFSET : (KS >= 6 ? 2 : 1);
             // every group's hand-off reads end before interval KS - 1
             static_assert(!STR2 || EO2 + ES2 * (NB - 1) <= KS - 2, "epilogue schedule overlaps the hand-off");
-            const bool str2 = STR2 && !(a.ablate & 64);
+            const bool str2 = STR2 && !(PMM_ABL(a.ablate) & 64);
             const int ES = str2 ? ES2 : 1;
             const int EO = str2 ? EO2 : 0;
             const int dks = KS == 1 ? 0 : (str2 ? (PMM_WS_DRAIN_INTERVAL >= 0 ? PMM_WS_DRAIN_INTERVAL % KS
@@ -642,7 +642,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
         }
       }
       barrier();  // the last tile's accumulators are in LDS
-      if (a.ablate != 1 && a.ablate != 3) {
+      if (PMM_ABL(a.ablate) != 1 && PMM_ABL(a.ablate) != 3) {
 #pragma unroll
         for (int c = 0; c < NB; c++) epilogue(t1 - 1, c);
         wait_lgkm0();

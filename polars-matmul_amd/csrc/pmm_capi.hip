@@ -54,8 +54,14 @@ struct DeviceInfo {
   int cus = 256;
   std::string arch;
 };
+constexpr int kMaxDevices = 64;
 std::mutex g_dev_mu;
-std::vector<DeviceInfo> g_dev;
+DeviceInfo g_dev[kMaxDevices];  // fixed storage: readers index it without the lock
+
+// Corpus sharding over several devices for the host entry points
+// (pmm_set_devices): process-wide, empty = one device.
+std::mutex g_devs_mu;
+std::vector<int> g_devs;
 
 struct TimingRec {
   const char *name;
@@ -94,6 +100,26 @@ struct DevScope {
   }
 };
 
+// Probes device `dev` once (gfx950 or a PMM_ERR_NODEVICE failure).
+int probe_device(int dev) {
+  if (dev < 0 || dev >= kMaxDevices) return fail(PMM_ERR_NODEVICE, "HIP device %d out of range", dev);
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  DeviceInfo &di = g_dev[dev];
+  if (!di.probed) {
+    hipDeviceProp_t p;
+    hipError_t e = hipGetDeviceProperties(&p, dev);
+    if (e != hipSuccess) return fail(PMM_ERR_NODEVICE, "no HIP device %d: %s", dev, hipGetErrorString(e));
+    di.probed = true;
+    di.arch = p.gcnArchName;
+    di.cus = p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
+    di.ok = di.arch.rfind("gfx950", 0) == 0;
+  }
+  if (!di.ok)
+    return fail(PMM_ERR_NODEVICE, "libpmm is built for gfx950 (MI355X); HIP device %d is %s", dev,
+                di.arch.c_str());
+  return PMM_OK;
+}
+
 // Device-pointer entry points (scope == NULL) run on the caller's current
 // device and leave it alone.  Host entry points pass a scope: they run on
 // `want` (a corpus handle's device), else on pmm_set_device's choice for this
@@ -103,24 +129,7 @@ int ensure_device(int *dev_out, DevScope *scope = nullptr, int want = -1) {
   HIP_TRY(hipGetDevice(&cur));
   int dev = cur;
   if (scope) dev = want >= 0 ? want : (t_ctx.device >= 0 ? t_ctx.device : cur);
-  {
-    std::lock_guard<std::mutex> lk(g_dev_mu);
-    if ((int)g_dev.size() <= dev) g_dev.resize(dev + 1);
-    DeviceInfo &di = g_dev[dev];
-    if (!di.probed) {
-      hipDeviceProp_t p;
-      hipError_t e = hipGetDeviceProperties(&p, dev);
-      if (e != hipSuccess)
-        return fail(PMM_ERR_NODEVICE, "no HIP device %d: %s", dev, hipGetErrorString(e));
-      di.probed = true;
-      di.arch = p.gcnArchName;
-      di.cus = p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
-      di.ok = di.arch.rfind("gfx950", 0) == 0;
-    }
-    if (!di.ok)
-      return fail(PMM_ERR_NODEVICE,
-                  "libpmm is built for gfx950 (MI355X); HIP device %d is %s", dev, di.arch.c_str());
-  }
+  if (int rc = probe_device(dev)) return rc;
   if (dev != cur) {
     HIP_TRY(hipSetDevice(dev));
     scope->prev = cur;
@@ -274,17 +283,6 @@ bool bf16_ws_enabled(int capg, int64_t d) {
   return capg <= kBf16WsMaxCapg && gemm_bf16_ws_lds_bytes(capg, dp) <= 160 * 1024;
 }
 
-// 256-query-row bf16 kernel (pmm_bf16_wide_kernel.h): opt-in (PMM_BF16_WIDE=1)
-// where its compaction holds the candidate buffer in registers (capg <= 384,
-// k <= 192).  Correct and bit-identical to the wave-specialised kernel, but
-// measured slower at c4, so not the default.  Read per call.
-bool bf16_wide_enabled(int capg, int64_t d) {
-  const char *e = getenv("PMM_BF16_WIDE");
-  if (!e || atoi(e) == 0) return false;
-  const int dp = (int)(cdiv(d, kBf16DAlign) * kBf16DAlign);
-  return capg <= kBf16WideMaxCapg && dp <= kBf16MaxD && gemm_bf16_wide_lds_bytes(dp) <= 160 * 1024;
-}
-
 // compute = PMM_COMPUTE_F32: the f32 kernel (variant chosen by LDS fit);
 // PMM_COMPUTE_BF16: the wave-specialised bf16 kernel (variant -2, 128 x 64
 // tiles, 8 waves) or the 4-wave one (variant -1, 128 x 128 tiles).
@@ -310,11 +308,10 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
     if (cap_env > 0 && k + 64 <= 512) p.capg = std::max<int>(((int)k + 64 + 7) / 8 * 8, std::min(cap_env, 512) / 8 * 8);
   }
   const bool bf16 = compute == PMM_COMPUTE_BF16;
-  const bool wide = bf16 && bf16_wide_enabled(p.capg, d);
-  const bool ws = bf16 && !wide && bf16_ws_enabled(p.capg, d);
-  p.variant = bf16 ? (wide ? -3 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
-  const int bm = bf16 ? (wide ? kBf16WideBM : kBf16BM) : gemm_f32_bm(p.variant);
-  const int bn = bf16 ? (wide ? kBf16WideBN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
+  const bool ws = bf16 && bf16_ws_enabled(p.capg, d);
+  p.variant = bf16 ? (ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
+  const int bm = bf16 ? kBf16BM : gemm_f32_bm(p.variant);
+  const int bn = bf16 ? (ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
   const size_t cand_budget = size_t(8) << 30;
   int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
@@ -331,10 +328,8 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   // f32 kernel: the same split of units (PMM_F32_WHOLE=0: split units only).
   // At c3 the GEMM time is unchanged (1076 ms either way) and the merge reads
   // 0.89 GB instead of 2.17 GB (0.40 vs 0.65 ms).
-  const bool whole = bf16 ? ((ws || wide) && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
-  // unit overhead in tiles: a wide unit's query-row load (256 rows x D) is
-  // about ten of its 32-column tiles
-  plan_units(m, n, bm, bn, cus, bf16 ? (wide ? 10.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
+  const bool whole = bf16 ? (ws && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
+  plan_units(m, n, bm, bn, cus, bf16 ? (ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
   // merge_kernel's per-row LDS capacity: at least 512, so a row's candidate
   // lists rarely need a compaction before the final one (c1: ~400 survivors
   // of the seed threshold per row; P = 128 compacted ~6 times, 23 us)
@@ -485,10 +480,12 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
   a.units = (int)units;
   a.qb_full = p.qb_full;
   a.counter = (unsigned *)(w + p.off_counter);
+#ifdef PMM_LAB
   {
     static const int ablate = getenv("PMM_ABLATE") ? atoi(getenv("PMM_ABLATE")) : 0;
     a.ablate = ablate;
   }
+#endif
   a.cand = (unsigned long long *)(w + p.off_cand);
   a.wq = (unsigned long long *)(w + p.off_wq);
   a.cnt = (unsigned *)(w + p.off_cnt);
@@ -511,10 +508,12 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
   ma.index_base = index_base;
   ma.out_idx = out_idx;
   ma.out_score = out_score;
+#ifdef PMM_LAB
   {
     static const int ablate = getenv("PMM_MERGE_ABLATE") ? atoi(getenv("PMM_MERGE_ABLATE")) : 0;
     ma.ablate = ablate;
   }
+#endif
   Timed t(merge_label, s);
   return launch_merge(ma, 0, s);
 }
@@ -720,10 +719,12 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
   a.ntiles = p.T;
   a.units = p.units;
   a.counter = (unsigned *)(w + p.off_counter);
+#ifdef PMM_LAB
   {
     static const int ablate = getenv("PMM_ABLATE") ? atoi(getenv("PMM_ABLATE")) : 0;
     a.ablate = ablate;
   }
+#endif
   a.cand = (unsigned long long *)(w + p.off_cand);
   a.wq = (unsigned long long *)(w + p.off_wq);
   a.cnt = (unsigned *)(w + p.off_cnt);
@@ -741,7 +742,11 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     static const int tmo_env =
         getenv("PMM_BF16_SYNC_TIMEOUT_US") ? atoi(getenv("PMM_BF16_SYNC_TIMEOUT_US")) : 20000;
     a.sync_timeout = tmo_env * 100;
+#ifdef PMM_LAB
     static const bool stats = getenv("PMM_STATS") != nullptr;
+#else
+    constexpr bool stats = false;  // (per-phase cycle counters: lab build only)
+#endif
     static unsigned long long *stats_buf = nullptr;
     if (stats) {
       if (!stats_buf) HIP_TRY(hipMalloc(&stats_buf, 128));
@@ -768,9 +773,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     }
     {
       Timed t("gemm_bf16_topk", s);
-      HIP_TRY(p.variant == -3   ? launch_gemm_bf16_wide(a, p.grid, s)
-              : p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s)
-                                : launch_gemm_bf16(a, p.grid, s));
+      HIP_TRY(p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s) : launch_gemm_bf16(a, p.grid, s));
     }
     if (stats) {
       unsigned long long h[16];
@@ -877,34 +880,44 @@ int topk_f32_host_chunked(const float *q, int64_t m, const float *c, int64_t n, 
   char *b = (char *)base;
   uint32_t *li = (uint32_t *)(b + off_l);
   hipEvent_t ev[kChunks + 1] = {};
-  auto cleanup = [&]() {
+  // One exit for every failure after the copy stream may have work queued:
+  // the copy stream writes into the arena, so it is drained before the arena
+  // can be reused or grown (freed) by a later call, and the events are freed.
+  auto finish = [&](int code) {
+    if (code != PMM_OK) {
+      (void)hipStreamSynchronize(cs);
+      (void)hipStreamSynchronize(s);
+    }
     for (auto &e : ev)
       if (e) (void)hipEventDestroy(e);
+    return code;
   };
-  for (auto &e : ev)
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
-      cleanup();
-      return fail(PMM_ERR_HIP, "hipEventCreate failed");
-    }
+#define CHUNK_TRY(expr)                                                                   \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return finish(fail(PMM_ERR_HIP, "HIP error %s at %s:%d (%s)", hipGetErrorString(e_), \
+                         __FILE__, __LINE__, #expr));                                     \
+  } while (0)
+  for (auto &e : ev) CHUNK_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // the copy stream must not overwrite the arena before earlier compute on
   // the compute stream is done with it
   hipEvent_t ready = ev[kChunks];
-  HIP_TRY(hipEventRecord(ready, s));
-  HIP_TRY(hipStreamWaitEvent(cs, ready, 0));
-  if ((rc = upload_padded(b + off_q, q, m, d, dp, 4, cs))) return cleanup(), rc;
+  CHUNK_TRY(hipEventRecord(ready, s));
+  CHUNK_TRY(hipStreamWaitEvent(cs, ready, 0));
+  if ((rc = upload_padded(b + off_q, q, m, d, dp, 4, cs))) return finish(rc);
   for (int i = 0; i < kChunks; i++) {
     const int64_t lo = bnd[i], rows = bnd[i + 1] - bnd[i];
     // a pageable copy returns once staged: chunk i + 1 is copied while the
     // device computes chunk i
-    if ((rc = upload_padded(b + off_c + (size_t)lo * dp * 4, c + lo * d, rows, d, dp, 4, cs)))
-      return cleanup(), rc;
-    HIP_TRY(hipEventRecord(ev[i], cs));
-    HIP_TRY(hipStreamWaitEvent(s, ev[i], 0));
+    if ((rc = upload_padded(b + off_c + (size_t)lo * dp * 4, c + lo * d, rows, d, dp, 4, cs))) return finish(rc);
+    CHUNK_TRY(hipEventRecord(ev[i], cs));
+    CHUNK_TRY(hipStreamWaitEvent(s, ev[i], 0));
     rc = topk_f32_device_impl((const float *)(b + off_q), dp, m, (const float *)(b + off_c) + lo * dp, dp,
                               rows, d, k, metric, (uint32_t)lo, li + (size_t)i * 2 * m * k,
                               (float *)(li + (size_t)i * 2 * m * k + (size_t)m * k), b + off_w, ws_need, s,
                               dev, nullptr, i > 0);
-    if (rc) return cleanup(), rc;
+    if (rc) return finish(rc);
   }
   MergeArgs ma{};
   ma.in_idx = li;
@@ -921,24 +934,240 @@ int topk_f32_host_chunked(const float *q, int64_t m, const float *c, int64_t n, 
   ma.out_score = (float *)(b + off_s);
   {
     Timed t("merge_chunks", s);
-    HIP_TRY(launch_merge(ma, 1, s));
+    CHUNK_TRY(launch_merge(ma, 1, s));
   }
-  HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  cleanup();
-  return PMM_OK;
+  CHUNK_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  CHUNK_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  CHUNK_TRY(hipStreamSynchronize(s));
+#undef CHUNK_TRY
+  return finish(PMM_OK);
 }
+
+// ---------------------------------------------------------------------------
+// Corpus-sharded top-k over several devices from ONE host thread (the
+// drop-in boundary's multi-GPU path; pmm_set_devices).  SURVEY 8e's plan in
+// one process: the corpus is row-sharded (contiguous, sizes differ by <= 1),
+// every device gets the queries, runs the fused top-k on its shard with
+// index_base = the shard's first global row into a [2][m][k] block (index
+// plane, score plane), the blocks are copied peer-to-peer (xGMI) into the
+// root device's [G][2][m][k] buffer and k-way merged there in place
+// (merge_kernel, the same strided loader the RCCL-gathered lists use).  All
+// devices work concurrently: every launch is asynchronous on the device's own
+// stream of this thread; the root waits on per-shard events.  Each shard's
+// list is the exact top-k of its rows under the total order, so the merged
+// list equals the one-device result bit for bit.
+// ---------------------------------------------------------------------------
+struct ShardSrc {
+  int dev;
+  int64_t lo, rows;
+  const float *host;       // host corpus rows [lo, lo + rows), row stride d, or
+  const float *dev_rows;   // resident padded rows (stride dp) of a corpus handle
+  const float *dev_norms;  // with dev_rows: the handle's norms of this metric ([rows | rows factors])
+};
+
+std::mutex g_peer_mu;
+bool g_peer_tried[kMaxDevices][kMaxDevices];
+
+// Lets `dev` read `peer`'s memory directly (xGMI) when the platform allows;
+// a peer copy works either way, so failures are ignored.
+void enable_peer(int dev, int peer) {
+  if (dev == peer) return;
+  std::lock_guard<std::mutex> lk(g_peer_mu);
+  if (g_peer_tried[dev][peer]) return;
+  g_peer_tried[dev][peer] = true;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, dev, peer) == hipSuccess && can) (void)hipDeviceEnablePeerAccess(peer, 0);
+  (void)hipGetLastError();
+}
+
+int topk_sharded(const float *q, int64_t m, int64_t d, int64_t k, int metric, int compute,
+                 const std::vector<ShardSrc> &sh, uint32_t *out_idx, float *out_score) {
+  const int G = (int)sh.size();
+  int cur = 0;
+  HIP_TRY(hipGetDevice(&cur));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{cur};
+  const bool bf16 = compute == PMM_COMPUTE_BF16;
+  const int64_t dp = bf16 ? cdiv(d, kBf16DAlign) * kBf16DAlign : cdiv(d, 32) * 32;
+  const int root = sh[0].dev;
+  const size_t list_bytes = (size_t)2 * m * k * 4;
+  // per distinct device: the queries once, one workspace (its shards run in
+  // stream order), per shard the uploaded rows (host shards) and its list
+  struct DevPlan {
+    int dev;
+    hipStream_t s = nullptr;
+    char *base = nullptr;
+    size_t off_q = 0, off_qb = 0, off_ws = 0, ws_bytes = 0, total = 0;
+  };
+  std::vector<DevPlan> dps;
+  std::vector<int> plan_of(G);
+  std::vector<size_t> off_c(G), off_cb(G), off_list(G);
+  for (int g = 0; g < G; g++) {
+    int j = 0;
+    while (j < (int)dps.size() && dps[j].dev != sh[g].dev) j++;
+    if (j == (int)dps.size()) {
+      if (int rc = probe_device(sh[g].dev)) return rc;
+      DevPlan p;
+      p.dev = sh[g].dev;
+      dps.push_back(p);
+    }
+    plan_of[g] = j;
+  }
+  for (auto &p : dps) {
+    HIP_TRY(hipSetDevice(p.dev));
+    size_t off = 0;
+    p.off_q = off;  // f32: padded rows; bf16: f32 staging rows (stride d)
+    off = al256(off + (size_t)m * (bf16 ? d : dp) * 4);
+    p.off_qb = off;  // bf16 rows
+    off = al256(off + (bf16 ? (size_t)m * dp * 2 : 0));
+    for (int g = 0; g < G; g++) {
+      if (sh[g].dev != p.dev) continue;
+      p.ws_bytes = std::max(p.ws_bytes, pmm_topk_workspace_bytes(m, sh[g].rows, dp, k, metric, compute));
+      off_c[g] = off;
+      if (sh[g].host) off = al256(off + (size_t)sh[g].rows * (bf16 ? d : dp) * 4);
+      off_cb[g] = off;
+      if (bf16) off = al256(off + (size_t)sh[g].rows * dp * 2);
+      off_list[g] = off;
+      off = al256(off + list_bytes);
+    }
+    p.off_ws = off;
+    off = al256(off + p.ws_bytes);
+    p.total = off;
+  }
+  // root: the gathered lists and the merged output
+  DevPlan &rp = dps[plan_of[0]];
+  const size_t off_gather = rp.total, off_out = al256(off_gather + (size_t)G * list_bytes);
+  rp.total = al256(off_out + list_bytes);
+  for (auto &p : dps) {
+    HIP_TRY(hipSetDevice(p.dev));
+    if (int rc = thread_stream(p.dev, &p.s)) return rc;
+    void *b;
+    if (int rc = arena(p.dev, p.s, p.total, &b)) return rc;
+    p.base = (char *)b;
+  }
+  std::vector<hipEvent_t> ev(G, nullptr);
+  auto finish = [&](int code) {
+    if (code != PMM_OK)
+      for (auto &p : dps) {
+        (void)hipSetDevice(p.dev);
+        (void)hipStreamSynchronize(p.s);
+      }
+    for (int g = 0; g < G; g++)
+      if (ev[g]) {
+        (void)hipSetDevice(sh[g].dev);
+        (void)hipEventDestroy(ev[g]);
+      }
+    return code;
+  };
+#define SH_TRY(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return finish(fail(PMM_ERR_HIP, "HIP error %s at %s:%d (%s)", hipGetErrorString(e_), \
+                         __FILE__, __LINE__, #expr));                                     \
+  } while (0)
+#define SH_RC(expr)                   \
+  do {                                \
+    int rc_ = (expr);                 \
+    if (rc_ != PMM_OK) return finish(rc_); \
+  } while (0)
+  // queries to every device
+  for (auto &p : dps) {
+    SH_TRY(hipSetDevice(p.dev));
+    if (bf16) {
+      SH_TRY(hipMemcpyAsync(p.base + p.off_q, q, (size_t)m * d * 4, hipMemcpyHostToDevice, p.s));
+      SH_TRY(launch_f32_to_bf16((const float *)(p.base + p.off_q), m, d, d, (uint16_t *)(p.base + p.off_qb), dp,
+                                p.s));
+    } else {
+      SH_RC(upload_padded(p.base + p.off_q, q, m, d, dp, 4, p.s));
+    }
+  }
+  // per shard: rows, fused top-k with global indices, completion event
+  for (int g = 0; g < G; g++) {
+    DevPlan &p = dps[plan_of[g]];
+    const ShardSrc &x = sh[g];
+    SH_TRY(hipSetDevice(p.dev));
+    SH_TRY(hipEventCreateWithFlags(&ev[g], hipEventDisableTiming));
+    uint32_t *li = (uint32_t *)(p.base + off_list[g]);
+    float *ls = (float *)(li + (size_t)m * k);
+    if (bf16) {
+      SH_TRY(hipMemcpyAsync(p.base + off_c[g], x.host, (size_t)x.rows * d * 4, hipMemcpyHostToDevice, p.s));
+      SH_TRY(launch_f32_to_bf16((const float *)(p.base + off_c[g]), x.rows, d, d,
+                                (uint16_t *)(p.base + off_cb[g]), dp, p.s));
+      SH_RC(topk_bf16_device_impl((const uint16_t *)(p.base + p.off_qb), dp, m,
+                                  (const uint16_t *)(p.base + off_cb[g]), dp, x.rows, d, k, metric,
+                                  (uint32_t)x.lo, li, ls, p.base + p.off_ws, p.ws_bytes, p.s, p.dev));
+    } else {
+      const float *c = x.dev_rows;
+      if (x.host) {
+        SH_RC(upload_padded(p.base + off_c[g], x.host, x.rows, d, dp, 4, p.s));
+        c = (const float *)(p.base + off_c[g]);
+      }
+      SH_RC(topk_f32_device_impl((const float *)(p.base + p.off_q), dp, m, c, dp, x.rows, d, k, metric,
+                                 (uint32_t)x.lo, li, ls, p.base + p.off_ws, p.ws_bytes, p.s, p.dev,
+                                 x.host ? nullptr : x.dev_norms));
+    }
+    SH_TRY(hipEventRecord(ev[g], p.s));
+  }
+  // gather into the root (peer copies over xGMI), merge, download
+  SH_TRY(hipSetDevice(root));
+  char *gb = rp.base + off_gather;
+  for (int g = 0; g < G; g++) {
+    enable_peer(root, sh[g].dev);
+    SH_TRY(hipStreamWaitEvent(rp.s, ev[g], 0));
+    SH_TRY(hipMemcpyPeerAsync(gb + (size_t)g * list_bytes, root, dps[plan_of[g]].base + off_list[g], sh[g].dev,
+                              list_bytes, rp.s));
+  }
+  MergeArgs ma{};
+  ma.in_idx = (const uint32_t *)gb;
+  ma.in_score = (const float *)((const uint32_t *)gb + (size_t)m * k);
+  ma.k_in = (int)k;
+  ma.row_stride = k;
+  ma.list_stride = 2 * m * k;
+  ma.M = (int)m;
+  ma.S = G;
+  ma.k_out = (int)k;
+  ma.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
+  ma.metric = metric;
+  ma.out_idx = (uint32_t *)(rp.base + off_out);
+  ma.out_score = (float *)(ma.out_idx + (size_t)m * k);
+  {
+    Timed t("merge_devices", rp.s);
+    SH_TRY(launch_merge(ma, 1, rp.s));
+  }
+  SH_TRY(hipMemcpyAsync(out_idx, ma.out_idx, (size_t)m * k * 4, hipMemcpyDeviceToHost, rp.s));
+  SH_TRY(hipMemcpyAsync(out_score, ma.out_score, (size_t)m * k * 4, hipMemcpyDeviceToHost, rp.s));
+  SH_TRY(hipStreamSynchronize(rp.s));
+#undef SH_TRY
+#undef SH_RC
+  return finish(PMM_OK);
+}
+
+std::vector<int> devices_snapshot() {
+  std::lock_guard<std::mutex> lk(g_devs_mu);
+  return g_devs;
+}
+
+// shard g of n rows over G shards: rows [n g / G, n (g + 1) / G)
+int64_t shard_lo(int64_t n, int G, int g) { return n * g / G; }
 
 }  // namespace
 
 // Device-resident corpus (pmm_corpus_*): padded f32 rows in HBM plus the
 // norms / pre-filter factors of every metric, computed once at creation.
-struct pmm_corpus {
+// With a device list set (pmm_set_devices) the rows are sharded over the
+// devices at creation, one contiguous shard each.
+struct CorpusShard {
   int device = 0;
-  int64_t n = 0, d = 0, dp = 0;
+  int64_t lo = 0, n = 0;    // rows [lo, lo + n) of the corpus
   float *data = nullptr;    // n x dp
   float *norms = nullptr;   // [cosine: n norms | n 1/norm][euclid: n sq | n sq*(1-2^-18)]
+};
+struct pmm_corpus {
+  int64_t n = 0, d = 0, dp = 0;
+  std::vector<CorpusShard> shards;
 };
 
 // ===========================================================================
@@ -990,13 +1219,35 @@ int pmm_set_device(int device) {
   return PMM_OK;
 }
 
+int pmm_set_devices(const int *ids, int n) {
+  if (n < 0 || (n > 0 && !ids)) return fail(PMM_ERR_ARG, "bad device list (n=%d)", n);
+  int count = 0;
+  pmm_device_count(&count);
+  for (int i = 0; i < n; i++)
+    if (ids[i] < 0 || ids[i] >= count || ids[i] >= kMaxDevices)
+      return fail(PMM_ERR_NODEVICE, "no HIP device %d (%d visible)", ids[i], count);
+  for (int i = 0; i < n; i++)
+    if (int rc = probe_device(ids[i])) return rc;
+  std::lock_guard<std::mutex> lk(g_devs_mu);
+  g_devs.assign(ids, ids + n);
+  return PMM_OK;
+}
+
+int pmm_get_devices(int *ids, int cap, int *n) {
+  if (!n || cap < 0 || (cap > 0 && !ids)) return fail(PMM_ERR_ARG, "null argument");
+  std::lock_guard<std::mutex> lk(g_devs_mu);
+  *n = (int)g_devs.size();
+  for (int i = 0; i < (int)g_devs.size() && i < cap; i++) ids[i] = g_devs[i];
+  return PMM_OK;
+}
+
 size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int metric,
                                 int compute) {
   int cus = 256;
   int dev = 0;
   if (hipGetDevice(&dev) == hipSuccess) {
     std::lock_guard<std::mutex> lk(g_dev_mu);
-    if ((int)g_dev.size() > dev && g_dev[dev].probed) cus = g_dev[dev].cus;
+    if (dev >= 0 && dev < kMaxDevices && g_dev[dev].probed) cus = g_dev[dev].cus;
   }
   if (compute == PMM_COMPUTE_BF16) {
     Plan p;
@@ -1026,7 +1277,7 @@ int pmm_topk_merge_bytes(const void *workspace, int64_t m, int64_t n, int64_t d,
   int cus = 256;
   {
     std::lock_guard<std::mutex> lk(g_dev_mu);
-    if ((int)g_dev.size() > dev && g_dev[dev].probed) cus = g_dev[dev].cus;
+    if (dev >= 0 && dev < kMaxDevices && g_dev[dev].probed) cus = g_dev[dev].cus;
   }
   Plan p;
   plan_topk(m, n, d, k, metric, cus, p, compute);
@@ -1082,6 +1333,20 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
   if (compute == PMM_COMPUTE_BF16 && (rc = bf16_limits(d, k, n))) return rc;
+  {
+    // a device list (pmm_set_devices): the corpus row-sharded over it, one
+    // shard per listed device (at most n shards), results merged on the first
+    const std::vector<int> devs = devices_snapshot();
+    if (devs.size() > 1 && k <= kFusedMaxK) {
+      const int G = (int)std::min<int64_t>((int64_t)devs.size(), n);
+      std::vector<ShardSrc> sh(G);
+      for (int g = 0; g < G; g++) {
+        const int64_t lo = shard_lo(n, G, g), hi = shard_lo(n, G, g + 1);
+        sh[g] = ShardSrc{devs[g], lo, hi - lo, c + lo * d, nullptr, nullptr};
+      }
+      return topk_sharded(q, m, d, k, metric, compute, sh, out_idx, out_score);
+    }
+  }
   int dev;
   DevScope scope;
   if ((rc = ensure_device(&dev, &scope))) return rc;
@@ -1371,31 +1636,47 @@ int pmm_corpus_create_f32(const float *c, int64_t n, int64_t d, pmm_corpus **out
   int dev;
   DevScope scope;
   if ((rc = ensure_device(&dev, &scope))) return rc;
-  hipStream_t s;
-  if ((rc = thread_stream(dev, &s))) return rc;
+  std::vector<int> devs = devices_snapshot();
+  if (devs.size() <= 1) devs.assign(1, dev);
+  const int G = (int)std::min<int64_t>((int64_t)devs.size(), n);
   pmm_corpus *h = new pmm_corpus();
-  h->device = dev;
   h->n = n;
   h->d = d;
   h->dp = cdiv(d, 32) * 32;
-  hipError_t e = hipMalloc(&h->data, (size_t)n * h->dp * 4);
-  if (e == hipSuccess) e = hipMalloc(&h->norms, (size_t)n * 4 * 4);
-  if (e != hipSuccess) {
-    if (h->data) (void)hipFree(h->data);
-    delete h;
-    return fail(PMM_ERR_HIP, "corpus allocation failed: %s", hipGetErrorString(e));
+  h->shards.resize(G);
+  for (int g = 0; g < G; g++) {
+    CorpusShard &x = h->shards[g];
+    x.device = devs[g];
+    x.lo = shard_lo(n, G, g);
+    x.n = shard_lo(n, G, g + 1) - x.lo;
   }
-  if ((rc = upload_padded(h->data, c, n, d, h->dp, 4, s))) {
-    pmm_corpus_destroy(h);
-    return rc;
+  for (int g = 0; g < G; g++) {
+    CorpusShard &x = h->shards[g];
+    hipStream_t s;
+    hipError_t e = hipSetDevice(x.device);
+    if (e == hipSuccess && (rc = thread_stream(x.device, &s))) {
+      pmm_corpus_destroy(h);
+      return rc;
+    }
+    if (e == hipSuccess) e = hipMalloc(&x.data, (size_t)x.n * h->dp * 4);
+    if (e == hipSuccess) e = hipMalloc(&x.norms, (size_t)x.n * 4 * 4);
+    if (e != hipSuccess) {
+      pmm_corpus_destroy(h);
+      return fail(PMM_ERR_HIP, "corpus allocation failed on device %d: %s", x.device, hipGetErrorString(e));
+    }
+    if ((rc = upload_padded(x.data, c + x.lo * d, x.n, d, h->dp, 4, s))) {
+      pmm_corpus_destroy(h);
+      return rc;
+    }
+    hipError_t e1 = launch_norms_f32(x.data, x.n, d, h->dp, 0, x.norms, x.norms + x.n, s);
+    hipError_t e2 = launch_norms_f32(x.data, x.n, d, h->dp, 1, x.norms + 2 * x.n, x.norms + 3 * x.n, s);
+    hipError_t e3 = hipStreamSynchronize(s);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+      pmm_corpus_destroy(h);
+      return fail(PMM_ERR_HIP, "corpus norms failed");
+    }
   }
-  hipError_t e1 = launch_norms_f32(h->data, n, d, h->dp, 0, h->norms, h->norms + n, s);
-  hipError_t e2 = launch_norms_f32(h->data, n, d, h->dp, 1, h->norms + 2 * n, h->norms + 3 * n, s);
-  hipError_t e3 = hipStreamSynchronize(s);
-  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
-    pmm_corpus_destroy(h);
-    return fail(PMM_ERR_HIP, "corpus norms failed");
-  }
+  (void)hipSetDevice(dev);
   *out = h;
   return PMM_OK;
 }
@@ -1404,10 +1685,13 @@ int pmm_corpus_destroy(pmm_corpus *h) {
   if (!h) return PMM_OK;
   int cur = 0;
   (void)hipGetDevice(&cur);
-  (void)hipSetDevice(h->device);
-  (void)hipDeviceSynchronize();
-  if (h->data) (void)hipFree(h->data);
-  if (h->norms) (void)hipFree(h->norms);
+  for (auto &x : h->shards) {
+    if (!x.data && !x.norms) continue;
+    (void)hipSetDevice(x.device);
+    (void)hipDeviceSynchronize();
+    if (x.data) (void)hipFree(x.data);
+    if (x.norms) (void)hipFree(x.norms);
+  }
   (void)hipSetDevice(cur);
   delete h;
   return PMM_OK;
@@ -1417,7 +1701,13 @@ int pmm_corpus_info(const pmm_corpus *h, int64_t *n, int64_t *d, int *device) {
   if (!h) return fail(PMM_ERR_ARG, "null corpus");
   if (n) *n = h->n;
   if (d) *d = h->d;
-  if (device) *device = h->device;
+  if (device) *device = h->shards.empty() ? -1 : h->shards[0].device;
+  return PMM_OK;
+}
+
+int pmm_corpus_shards(const pmm_corpus *h, int *shards) {
+  if (!h || !shards) return fail(PMM_ERR_ARG, "null argument");
+  *shards = (int)h->shards.size();
   return PMM_OK;
 }
 
@@ -1428,9 +1718,25 @@ int pmm_topk_f32_corpus(const pmm_corpus *h, const float *q, int64_t m, int64_t 
   if (rc) return rc;
   if ((rc = check_metric(metric))) return rc;
   if (m == 0 || k == 0) return PMM_OK;
+  // which of a shard's norm arrays this metric reads (none for dot)
+  auto shard_norms = [&](const CorpusShard &x) -> const float * {
+    return metric == kMetricCosine ? x.norms : metric == kMetricEuclidean ? x.norms + 2 * x.n : nullptr;
+  };
+  if (h->shards.size() > 1 && k <= kFusedMaxK) {
+    std::vector<ShardSrc> sh(h->shards.size());
+    for (size_t g = 0; g < sh.size(); g++) {
+      const CorpusShard &x = h->shards[g];
+      sh[g] = ShardSrc{x.device, x.lo, x.n, nullptr, x.data, shard_norms(x)};
+    }
+    return topk_sharded(q, m, h->d, k, metric, PMM_COMPUTE_F32, sh, out_idx, out_score);
+  }
+  if (h->shards.size() > 1)
+    return fail(PMM_ERR_UNSUPPORTED, "a device-sharded corpus supports k <= %d (got %lld)", kFusedMaxK,
+                (long long)k);
+  const CorpusShard &x = h->shards[0];
   int dev;
   DevScope scope;
-  if ((rc = ensure_device(&dev, &scope, h->device))) return rc;
+  if ((rc = ensure_device(&dev, &scope, x.device))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   const int64_t dp = h->dp;
@@ -1441,11 +1747,9 @@ int pmm_topk_f32_corpus(const pmm_corpus *h, const float *q, int64_t m, int64_t 
   if ((rc = arena(dev, s, off_w + ws_need, &base))) return rc;
   char *b = (char *)base;
   if ((rc = upload_padded(b + off_q, q, m, h->d, dp, 4, s))) return rc;
-  const float *cn = metric == kMetricCosine ? h->norms
-                    : metric == kMetricEuclidean ? h->norms + 2 * h->n : nullptr;
-  rc = topk_f32_device_impl((const float *)(b + off_q), dp, m, h->data, dp, h->n, h->d, k, metric,
+  rc = topk_f32_device_impl((const float *)(b + off_q), dp, m, x.data, dp, h->n, h->d, k, metric,
                             0u, (uint32_t *)(b + off_i), (float *)(b + off_s), b + off_w, ws_need,
-                            s, dev, cn);
+                            s, dev, shard_norms(x));
   if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));

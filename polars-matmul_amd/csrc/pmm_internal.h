@@ -7,6 +7,16 @@
 
 namespace pmm {
 
+// Benchmarking-only phase removal (PMM_ABLATE / PMM_MERGE_ABLATE: results are
+// wrong by design).  Compiled in only by the lab build (`make lab` ->
+// libpmm_lab.so, -DPMM_LAB); in the shipped libpmm.so the variables are never
+// read and every ablation branch folds away at compile time.
+#ifdef PMM_LAB
+#define PMM_ABL(x) (x)
+#else
+#define PMM_ABL(x) 0
+#endif
+
 constexpr int kMetricCosine = 0;
 constexpr int kMetricDot = 1;
 constexpr int kMetricEuclidean = 2;
@@ -133,17 +143,6 @@ hipError_t launch_gemm_bf16_ws(const GemmF32Args &a, int grid, hipStream_t s);
 // bf16 threshold seed (pmm_bf16_ws_kernel.h): S[row][0..ns) = the scores of
 // corpus rows 0..ns-1 exactly as the wave-specialised kernel computes them
 hipError_t launch_seed_bf16_ws(const GemmF32Args &a, float *S, int ns, hipStream_t s);
-// 256-query-row bf16 kernel (pmm_bf16_wide_kernel.h): 8 waves (2 per SIMD),
-// each 32 query rows x D in registers, 32-column corpus tiles; used when capg
-// <= kBf16WideMaxCapg unless PMM_BF16_WIDE=0.
-constexpr int kBf16WideBM = 256, kBf16WideBN = 32;
-constexpr int kBf16WideMaxCapg = 384;  // k <= 192 (the compaction's registers)
-#ifndef PMM_BF16_WIDE_AHEAD
-#define PMM_BF16_WIDE_AHEAD 6
-#endif
-constexpr int kBf16WideAhead = PMM_BF16_WIDE_AHEAD;  // K-steps of corpus DMA in flight
-size_t gemm_bf16_wide_lds_bytes(int D);  // D = padded dimension
-hipError_t launch_gemm_bf16_wide(const GemmF32Args &a, int grid, hipStream_t s);
 // f32 rows -> bf16 (round to nearest even) with row stride ldd, columns
 // d..ldd-1 zero-filled.
 hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t lds, uint16_t *dst,

@@ -395,7 +395,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       rb = rbn;
 
       const int col0 = tile * G::BN;
-      if (a.ablate == 1) {
+      if (PMM_ABL(a.ablate) == 1) {
         // ablation build path: keep the accumulators live, skip the epilogue
         float sink = 0.0f;
 #pragma unroll
@@ -462,14 +462,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             const bool p = cvalid && !(pv < lo[e]);
             const u64 m = __ballot(p);
             if (m == 0ull) continue;
-            if (p && a.ablate != 2) {
+            if (p && PMM_ABL(a.ablate) != 2) {
               const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
               gq[qlen + lanes_below(m)] = (u64)__float_as_uint(v) | ((u64)hi << 32);
             }
             qlen += __popcll(m);
           }
         }
-        if (a.ablate == 2) qlen = 0;  // ablation: pre-filter only
+        if (PMM_ABL(a.ablate) == 2) qlen = 0;  // ablation: pre-filter only
         if (qlen) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // queue stores reached L2
           for (int base = 0; base < qlen; base += 64) {
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
       cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
     }
   };
-  if (a.ablate == 2) {
+  if (PMM_ABL(a.ablate) == 2) {
     // (benchmarking only: no candidate loads)
   } else if (a.S <= 64) {
     // All list lengths in one load (lane s holds list s's), then the lists'
@@ -666,7 +666,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     }
   }
   wave_sync();
-  if (a.ablate != 1) {
+  if (PMM_ABL(a.ablate) != 1) {
     if (cnt > a.k_out && a.P <= 512) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
     const int P2 = min(a.P, next_pow2_dev(cnt));
     for (int i = cnt + lane; i < P2; i += 64) scr[i] = 0ull;

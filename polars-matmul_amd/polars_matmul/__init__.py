@@ -16,6 +16,12 @@ Usage:
 Without Polars, the same extension functions accept pyarrow arrays or numpy
 matrices (``polars_matmul._polars_matmul._topk``), and ``topk`` / ``matmul``
 below are numpy-level conveniences.
+
+Multi-GPU (an extension; the reference is single-process): ``set_devices([0,
+1, ..., 7])`` -- or ``PMM_DEVICES=all`` / ``PMM_DEVICES=0,1,2,3`` in the
+environment -- row-shards the corpus of every later ``.pmm.topk`` over those
+GPUs inside the one Polars process and merges the per-GPU lists on the first
+(include/pmm.h ``pmm_set_devices``); results are identical to one GPU's.
 """
 from __future__ import annotations
 
@@ -27,11 +33,13 @@ from polars_matmul._polars_matmul import (  # noqa: F401
     PanicException,
     _matmul,
     _topk,
+    get_devices,
+    set_devices,
 )
 from polars_matmul import _native
 
 __version__ = "0.1.4"
-__all__ = ["PmmNamespace", "topk", "matmul"]
+__all__ = ["PmmNamespace", "topk", "matmul", "set_devices", "get_devices"]
 
 Metric = Literal["cosine", "dot", "euclidean"]
 Compute = Literal["f32", "bf16"]

@@ -45,6 +45,8 @@ EXPORTED_SYMBOLS = (
     "pmm_device_count",
     "pmm_device_memory",
     "pmm_set_device",
+    "pmm_set_devices",
+    "pmm_get_devices",
     "pmm_topk_f32",
     "pmm_topk_f32_ex",
     "pmm_topk_f64",
@@ -61,6 +63,7 @@ EXPORTED_SYMBOLS = (
     "pmm_corpus_create_f32",
     "pmm_corpus_destroy",
     "pmm_corpus_info",
+    "pmm_corpus_shards",
     "pmm_topk_f32_corpus",
     "pmm_timing_enable",
     "pmm_timing_reset",
@@ -112,6 +115,8 @@ _SIGS = {
     "pmm_device_count": ([ctypes.POINTER(ctypes.c_int)], _i32),
     "pmm_device_memory": ([ctypes.POINTER(_sz), ctypes.POINTER(_sz)], _i32),
     "pmm_set_device": ([_i32], _i32),
+    "pmm_set_devices": ([ctypes.POINTER(ctypes.c_int), _i32], _i32),
+    "pmm_get_devices": ([ctypes.POINTER(ctypes.c_int), _i32, ctypes.POINTER(ctypes.c_int)], _i32),
     "pmm_topk_f32": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_topk_f32_ex": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _i32, _vp, _vp], _i32),
     "pmm_topk_f64": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
@@ -137,6 +142,7 @@ _SIGS = {
         [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)],
         _i32,
     ),
+    "pmm_corpus_shards": ([_vp, ctypes.POINTER(ctypes.c_int)], _i32),
     "pmm_topk_f32_corpus": ([_vp, _vp, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_timing_enable": ([_i32], _i32),
     "pmm_timing_reset": ([], _i32),
@@ -191,6 +197,24 @@ def device_memory():
     f, t = _sz(0), _sz(0)
     check(_lib.pmm_device_memory(ctypes.byref(f), ctypes.byref(t)))
     return f.value, t.value
+
+
+def set_devices(ids) -> None:
+    """Row-shard the corpus of later host top-k calls (and corpus handles
+    created afterwards) over these HIP devices, results merged on ids[0]
+    (pmm_set_devices).  An empty list returns to one device."""
+    ids = [int(i) for i in ids]
+    arr = (ctypes.c_int * max(1, len(ids)))(*ids)
+    check(_lib.pmm_set_devices(arr, len(ids)))
+
+
+def get_devices():
+    """The current device list (pmm_get_devices); [] = one device."""
+    n = ctypes.c_int(0)
+    check(_lib.pmm_get_devices(None, 0, ctypes.byref(n)))
+    arr = (ctypes.c_int * max(1, n.value))()
+    check(_lib.pmm_get_devices(arr, n.value, ctypes.byref(n)))
+    return list(arr[:n.value])
 
 
 def metric_from_str(s: str) -> int:
@@ -292,6 +316,14 @@ def timing_read(kernel: str):
     return ms.value, n.value
 
 
+def corpus_device_bytes(n: int, d: int) -> int:
+    """HBM a DeviceCorpus of n x d f32 rows holds (pmm_corpus_create_f32): the
+    rows padded to a multiple of 32 floats plus four norm arrays (cosine norms
+    and pre-filter factors, euclidean squared norms and factors)."""
+    dp = -(-d // 32) * 32
+    return n * dp * 4 + n * 4 * 4
+
+
 class DeviceCorpus:
     """An f32 corpus uploaded once to HBM with its norms (pmm_corpus_*).
 
@@ -309,7 +341,7 @@ class DeviceCorpus:
         self._refs = 0
         self._closing = False
         self.n, self.d = c.shape
-        self.nbytes = c.nbytes
+        self.nbytes = corpus_device_bytes(self.n, self.d)  # device footprint, not host bytes
 
     def acquire(self) -> "DeviceCorpus":
         with self._lock:
@@ -342,6 +374,13 @@ class DeviceCorpus:
         if self._h:
             _lib.pmm_corpus_destroy(self._h)
             self._h = ctypes.c_void_p()
+
+    @property
+    def shards(self) -> int:
+        """Device shards of this corpus (pmm_corpus_shards)."""
+        n = ctypes.c_int(0)
+        check(_lib.pmm_corpus_shards(self._h, ctypes.byref(n)))
+        return n.value
 
     @property
     def closed(self) -> bool:

@@ -216,18 +216,29 @@ def _arrow_key(arr):
 def _cached_corpus(original, rv, c: np.ndarray):
     """An ACQUIRED DeviceCorpus for this corpus (the caller releases it), or
     None when the corpus is not cacheable."""
-    if not (_is_polars_series(original) or isinstance(original, pa.Array)
-            or (isinstance(original, pa.ChunkedArray) and original.num_chunks == 1)):
+    # Only inputs whose Arrow buffers persist across calls: a single-chunk
+    # Polars Series (rechunk() then returns the same buffers; a multi-chunk
+    # one is concatenated into a fresh buffer on every call, whose address
+    # key would never hit while each miss pinned host and device memory), an
+    # Arrow array, or a single-chunk ChunkedArray.
+    if _is_polars_series(original):
+        if original.n_chunks() != 1:
+            return None
+    elif not (isinstance(original, pa.Array)
+              or (isinstance(original, pa.ChunkedArray) and original.num_chunks == 1)):
         return None
     key = _arrow_key(rv)
-    if not _CACHE_ON or key is None or c.nbytes < _CACHE_MIN_BYTES or c.nbytes > _CACHE_BYTES:
+    if key is not None:
+        key = key + (tuple(_native.get_devices()),)  # a handle is sharded over the list of its creation
+    dev_bytes = _native.corpus_device_bytes(c.shape[0], c.shape[1])
+    if not _CACHE_ON or key is None or c.nbytes < _CACHE_MIN_BYTES or dev_bytes > _CACHE_BYTES:
         return None
     with _cache_lock:
         hit = _cache.get(key)
         if hit is not None:
             _cache.move_to_end(key)
             return hit[1].acquire()
-        if not _fits_device(c.nbytes):
+        if not _fits_device(dev_bytes):
             return None
         dc = _native.DeviceCorpus(c)
         _cache[key] = (rv, dc)
@@ -244,6 +255,45 @@ def clear_corpus_cache() -> None:
         while _cache:
             _, (_, dc) = _cache.popitem()
             dc.close()
+
+
+# ---------------------------------------------------------------------------
+# Device list (multi-GPU through the drop-in: include/pmm.h pmm_set_devices).
+# PMM_DEVICES = "all" or a comma list is applied on the first top-k call (not
+# at import: counting devices initialises the HIP runtime).
+# ---------------------------------------------------------------------------
+_devices_env_done = False
+
+
+def _parse_devices(spec: str, count: int):
+    spec = spec.strip().lower()
+    if spec in ("", "0-0"):
+        return []
+    if spec == "all":
+        return list(range(count))
+    return [int(x) for x in spec.split(",") if x.strip()]
+
+
+def _apply_devices_env() -> None:
+    global _devices_env_done
+    if _devices_env_done:
+        return
+    _devices_env_done = True
+    spec = os.environ.get("PMM_DEVICES")
+    if spec:
+        set_devices(_parse_devices(spec, _native.device_count()))
+
+
+def set_devices(ids) -> None:
+    """Row-shard the corpus of later top-k calls over these GPUs (results
+    merged on the first, identical to one GPU's); [] = one GPU."""
+    global _devices_env_done
+    _devices_env_done = True  # an explicit choice overrides PMM_DEVICES
+    _native.set_devices(list(ids))
+
+
+def get_devices():
+    return _native.get_devices()
 
 
 # ---------------------------------------------------------------------------
@@ -297,7 +347,9 @@ def _topk(left, right, k, metric):
         idx = np.zeros((m, 0), dtype=np.uint32)
         sc = np.zeros((m, 0), dtype=np.float64)
     else:
-        dc = _cached_corpus(right, rv, c) if use_f32 else None
+        _apply_devices_env()
+        # (a device-sharded handle serves k <= 1024; larger k runs on one GPU)
+        dc = _cached_corpus(right, rv, c) if use_f32 and (kk <= 1024 or not _native.get_devices()) else None
         if dc is not None:
             try:
                 idx, sc = dc.topk(q, kk, metric_id)
@@ -329,4 +381,4 @@ def _matmul(left, right):
     return _wrap(arr, "matmul", polars_out)
 
 
-__all__ = ["_matmul", "_topk", "PanicException", "clear_corpus_cache"]
+__all__ = ["_matmul", "_topk", "PanicException", "clear_corpus_cache", "set_devices", "get_devices"]

@@ -267,3 +267,75 @@ def test_corpus_cache_respects_free_device_memory(monkeypatch):
     dc = pm._cached_corpus(arr, arr, c)
     assert dc is created[0] and len(pm._cache) == 1
     assert pm._cached_corpus(arr, arr, c) is dc and len(created) == 1  # hit
+
+
+def test_corpus_cache_skips_multi_chunk_polars_series(monkeypatch):
+    # a multi-chunk Polars Series is concatenated into a
+    # fresh buffer by every rechunk(), so its address key never hits -- it
+    # must not be cached at all (no entry, no device upload per call)
+    from polars_matmul import _polars_matmul as pm
+
+    created = []
+
+    class StubCorpus:
+        def __init__(self, c):
+            self.nbytes = c.nbytes
+            created.append(self)
+
+        def acquire(self):
+            return self
+
+        def close(self):
+            pass
+
+    c = np.zeros((4096, 128), dtype=np.float32)
+    arr = pa.FixedSizeListArray.from_arrays(pa.array(c.reshape(-1)), 128)
+
+    class FakeSeries:
+        def __init__(self, chunks):
+            self.chunks = chunks
+
+        def n_chunks(self):
+            return self.chunks
+
+        def rechunk(self):
+            return self
+
+        def to_arrow(self):
+            return arr
+
+    monkeypatch.setattr(pm, "_is_polars_series", lambda o: isinstance(o, FakeSeries))
+    monkeypatch.setattr(_native, "DeviceCorpus", StubCorpus)
+    monkeypatch.setattr(_native, "device_memory", lambda: (1 << 40, 1 << 40))
+    monkeypatch.setattr(pm, "_CACHE_ON", True)
+    monkeypatch.setattr(pm, "_cache", collections.OrderedDict())
+    multi = FakeSeries(2)
+    for _ in range(2):
+        assert pm._cached_corpus(multi, arr, c) is None
+    assert created == [] and len(pm._cache) == 0
+    single = FakeSeries(1)
+    dc = pm._cached_corpus(single, arr, c)
+    assert dc is created[0] and len(pm._cache) == 1
+
+
+def test_corpus_cache_sizes_entries_by_device_footprint():
+    # the device holds rows padded to 32 floats plus four
+    # norm arrays, so d = 72 takes 96 floats per row on the device
+    assert _native.corpus_device_bytes(1000, 72) == 1000 * 96 * 4 + 1000 * 16
+    assert _native.corpus_device_bytes(10, 32) == 10 * 32 * 4 + 10 * 16
+
+
+def test_device_list_parse_and_validation():
+    # multi-GPU through the drop-in (include/pmm.h pmm_set_devices): the
+    # PMM_DEVICES spec, an empty list, and an invalid device id
+    from polars_matmul import _polars_matmul as pm
+
+    assert pm._parse_devices("all", 8) == list(range(8))
+    assert pm._parse_devices("0,1, 3", 8) == [0, 1, 3]
+    assert pm._parse_devices("", 8) == []
+    _native.set_devices([])
+    assert _native.get_devices() == []
+    with pytest.raises(_native.PmmError) as ei:
+        _native.set_devices([_native.device_count() + 5])
+    assert ei.value.code == _native.PMM_ERR_NODEVICE
+    assert _native.get_devices() == []

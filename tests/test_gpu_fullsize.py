@@ -158,8 +158,18 @@ def test_c4_fullsize_bf16(c3_data):
     elem = float(np.mean(idx[rows] == oi))
     print(f"c4 bf16 sample of {len(rows)} rows vs oracle on the rounded rows: strict row exact-match "
           f"{rate:.4f}, element match {elem:.4f}")
-    assert elem >= 0.95
+    # the bf16 MFMA sums in its own order: only near-ties (f32 accumulation
+    # order) may swap against the oracle's chain on the rounded rows
+    assert elem >= 0.995, f"c4 bf16: element match {elem:.4f} vs the oracle on the rounded rows"
     _check_lists(idx, sc, N, "c4 bf16")
+    # SURVEY 8c's bf16 bar on every row: recall@100 against the f32 lists of
+    # the same (unrounded) rows
+    fi, _ = _run_topk(q32, c32, K)
+    from bench import recall_at_k
+
+    rec = recall_at_k(idx, fi)
+    print(f"c4 bf16 recall@{K} vs the c3 f32 lists, all {M} rows: {rec:.4f}")
+    assert rec >= 0.95, rec
     resc = oracle.pair_scores(qh, ch, idx, oracle.COSINE, nthreads=THREADS)
     err = float(np.max(np.abs(resc.astype(np.float64) - sc)))
     assert err <= 1e-5, f"c4 bf16: max |score - oracle re-score| {err:.3g}"
@@ -212,3 +222,116 @@ def test_c5_shape_sharded_1m_bitexact():
     resc = oracle.pair_scores(qh, ch, got_i, oracle.COSINE, nthreads=THREADS)
     assert np.array_equal(resc.view(np.uint32), got_s.view(np.uint32))
     _check_nothing_better_outside(q, c, got_i, got_s, 1e-5, "c5-shape")
+
+
+def _oracle_topk_chunked(qh, c_dev, k, chunk=1 << 21):
+    """oracle.topk of a few query rows against a corpus too large to copy to
+    the host at once: the oracle over each corpus chunk (global indices), then
+    the best k of the chunk lists under the same total order (score desc, then
+    lower index) -- the oracle's result over the whole corpus, since each
+    chunk's list holds that chunk's top k."""
+    n = c_dev.shape[0]
+    idx, sc = [], []
+    for lo in range(0, n, chunk):
+        ch = c_dev[lo:lo + chunk].cpu().numpy()
+        oi, osc = oracle.topk(qh, ch, k, oracle.COSINE, nthreads=THREADS)
+        idx.append(oi.astype(np.int64) + lo)
+        sc.append(osc)
+        del ch
+    idx, sc = np.concatenate(idx, axis=1), np.concatenate(sc, axis=1)
+    order = np.lexsort((idx, -sc), axis=1)[:, :k]  # score desc, then index asc
+    return (np.take_along_axis(idx, order, axis=1).astype(np.uint32),
+            np.take_along_axis(sc, order, axis=1))
+
+
+def _pair_scores_chunked(qh, c_dev, idx):
+    """oracle.pair_scores over a device corpus, gathering only the corpus rows
+    the lists name (the full corpus need not cross to the host)."""
+    torch = _torch()
+    uniq, inv = np.unique(idx, return_inverse=True)
+    rows = c_dev[torch.from_numpy(uniq.astype(np.int64)).to(c_dev.device)].cpu().numpy()
+    return oracle.pair_scores(qh, rows, inv.reshape(idx.shape).astype(np.uint32), oracle.COSINE,
+                              nthreads=THREADS)
+
+
+def test_c5_full_corpus_10m_sharded_8way_bitexact():
+    # BASELINE configs[4] at its corpus size on one GPU: the full 10,000,000 x
+    # 1024 f32 corpus (41 GB, bench.synth_rows: the bench's own rows), 4096
+    # queries.  The 8 shard_bounds shards run through the per-rank path
+    # (fused top-k with index_base) and the rank-0 merge (_device_merge on the
+    # [world][2][m][k] gather layout); that equals the unsharded run bit for
+    # bit, a 24-row sample equals oracle.topk over the whole 10M corpus, and
+    # every returned pair equals its oracle re-score.
+    torch = _torch()
+    from polars_matmul.sharded import _device_merge, shard_bounds
+
+    dev = torch.device("cuda:0")
+    m, n, d, k, world = 4096, 10_000_000, 1024, 100, 8
+    q = _gen(m, d, QSEED, dev)
+    c = _gen(n, d, CSEED, dev)
+    full_i, full_s = _run_topk(q, c, k)
+    gathered = torch.empty((world, 2, m, k), dtype=torch.int32, device=dev)
+    for r in range(world):
+        a, b = shard_bounds(n, world, r)
+        li, ls = _run_topk(q, c[a:b], k, index_base=a)
+        gathered[r, 0] = torch.from_numpy(li.view(np.int32)).to(dev)
+        gathered[r, 1] = torch.from_numpy(ls.view(np.int32)).to(dev)
+    mi = torch.empty((m, k), dtype=torch.int32, device=dev)
+    ms = torch.empty((m, k), dtype=torch.float32, device=dev)
+    _device_merge(gathered, k, COS, mi, ms)
+    torch.cuda.synchronize()
+    got_i, got_s = mi.cpu().numpy().view(np.uint32), ms.cpu().numpy()
+    assert np.array_equal(got_i, full_i) and np.array_equal(got_s.view(np.uint32), full_s.view(np.uint32))
+    _check_lists(got_i, got_s, n, "c5 10M")
+    qh = q.cpu().numpy()
+    rows = np.linspace(0, m - 1, 24).astype(np.int64)
+    oi, osc = _oracle_topk_chunked(qh[rows], c, k)
+    assert np.array_equal(got_i[rows], oi)
+    assert np.array_equal(got_s[rows], osc.astype(np.float32))
+    resc = _pair_scores_chunked(qh, c, got_i)
+    assert np.array_equal(resc.view(np.uint32), got_s.view(np.uint32)), \
+        f"c5 10M: {int((resc != got_s).sum())} scores differ from the oracle re-score"
+    worst = _check_nothing_better_outside(q, c, got_i, got_s, 1e-5, "c5 10M", chunk=256)
+    print(f"c5 {m}x{n}x{d}: 8 shards + merge == unsharded; 24 rows == oracle over 10M; "
+          f"all {m * k} pairs == oracle re-score; best non-returned - kth <= {worst:.3g}")
+    del q, c, gathered
+    torch.cuda.empty_cache()
+
+
+def test_c5_per_rank_shape_one_launch():
+    # One launch of the per-GPU share of BASELINE configs[4] on 8 GPUs: all
+    # 1,000,000 queries against one 1,250,000-row shard (rows [0, 1.25M) of
+    # the bench corpus), D = 1024, k = 100 -- 2.56 PFLOP, ~18 s.  Every row:
+    # list properties and every returned pair equal to its oracle re-score; a
+    # 32-row sample equal to oracle.topk; no better row missed on a 65,536-row
+    # sample (torch f32 GEMM).  Prints the kernel time and MFMA fraction.
+    torch = _torch()
+    from polars_matmul import _native
+
+    dev = torch.device("cuda:0")
+    m, n, d, k = 1_000_000, 1_250_000, 1024, 100
+    q = _gen(m, d, QSEED, dev)
+    c = _gen(n, d, CSEED, dev)
+    _native.timing_reset()
+    _native.timing_enable(True)
+    idx, sc = _run_topk(q, c, k)
+    _native.timing_enable(False)
+    ms, launches = _native.timing_read("gemm_f32_topk")
+    tflops = 2.0 * m * n * d / (ms / 1000.0) / 1e12
+    print(f"c5 per-rank shape {m}x{n}x{d}: fused kernel {ms:.1f} ms ({launches} launch), "
+          f"{tflops:.1f} TFLOP/s = {tflops / 157.3:.3f} of the f32 MFMA peak")
+    _check_lists(idx, sc, n, "c5 per-rank")
+    qh, ch = q.cpu().numpy(), c.cpu().numpy()
+    resc = oracle.pair_scores(qh, ch, idx, oracle.COSINE, nthreads=THREADS)
+    assert np.array_equal(resc.view(np.uint32), sc.view(np.uint32)), \
+        f"c5 per-rank: {int((resc != sc).sum())} of {sc.size} scores differ from the oracle re-score"
+    rows = np.linspace(0, m - 1, 32).astype(np.int64)
+    oi, osc = oracle.topk(qh[rows], ch, k, oracle.COSINE, nthreads=THREADS)
+    assert np.array_equal(idx[rows], oi) and np.array_equal(sc[rows], osc.astype(np.float32))
+    del qh, ch
+    sub = torch.arange(0, m, m // 65536, device=dev)[:65536]
+    worst = _check_nothing_better_outside(q[sub], c, idx[sub.cpu().numpy()], sc[sub.cpu().numpy()], 1e-5,
+                                          "c5 per-rank")
+    print(f"c5 per-rank: all {m} rows re-scored bit-exact; best non-returned - kth <= {worst:.3g}")
+    del q, c
+    torch.cuda.empty_cache()

@@ -580,44 +580,11 @@ def test_bf16_one_wave_per_simd_kernel(pmm, m, n, d, k, metric, monkeypatch):
     # PMM_BF16_WS=0: the 4-wave kernel (pmm_bf16_kernel.h) on shapes the
     # wave-specialised kernel serves by default (it still serves k > 448)
     monkeypatch.setenv("PMM_BF16_WS", "0")
-    monkeypatch.setenv("PMM_BF16_WIDE", "0")
     rs = np.random.RandomState(m + n + d + k)
     q = rs.randn(m, d).astype(np.float32)
     c = rs.randn(n, d).astype(np.float32)
     idx, sc = gpu_topk_bf16(q, c, k, metric)
     _bf16_truth_check(q, c, k, metric, idx, sc, f"bf16 classic {m}x{n}x{d} k={k} {metric}")
-
-
-@pytest.mark.parametrize("m,n,d,k", [(130, 257, 33, 7), (257, 4099, 200, 64), (300, 2000, 768, 100),
-                                     (300, 2000, 768, 448)])
-@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-def test_bf16_wide_kernel(pmm, m, n, d, k, metric, monkeypatch):
-    # PMM_BF16_WIDE=1: the opt-in 256-row kernel (pmm_bf16_wide_kernel.h; k >
-    # 192 falls back to the wave-specialised kernel) vs float64 truth
-    monkeypatch.setenv("PMM_BF16_WIDE", "1")
-    rs = np.random.RandomState(m + n + d + k + 1)
-    q = rs.randn(m, d).astype(np.float32)
-    c = rs.randn(n, d).astype(np.float32)
-    idx, sc = gpu_topk_bf16(q, c, k, metric)
-    _bf16_truth_check(q, c, k, metric, idx, sc, f"bf16 wide {m}x{n}x{d} k={k} {metric}")
-
-
-@pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (520, 40000, 768, 100), (70, 3000, 640, 192)])
-@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-def test_bf16_wide_equals_wave_specialised(pmm, m, n, d, k, metric, monkeypatch):
-    # the 256-row kernel (corpus as the MFMA's A operand) and the 128-row
-    # kernel (queries as A) sum the same bf16 products in the same K order:
-    # identical f32 scores, so identical top-k lists, bit for bit
-    rs = np.random.RandomState(m + n + d + k + 2)
-    q = rs.randn(m, d).astype(np.float32)
-    c = rs.randn(n, d).astype(np.float32)
-    c[n // 2:n // 2 + 50] = c[:50]  # exact ties across the corpus
-    monkeypatch.setenv("PMM_BF16_WIDE", "0")
-    wi, ws_ = gpu_topk_bf16(q, c, k, metric)
-    monkeypatch.setenv("PMM_BF16_WIDE", "1")
-    gi, gs = gpu_topk_bf16(q, c, k, metric)
-    assert np.array_equal(gi, wi), f"{metric}: {np.mean(gi == wi)}"
-    assert np.array_equal(gs, ws_)
 
 
 @pytest.mark.parametrize("m,n,d", [(300, 20000, 768), (140, 9000, 200), (70, 8200, 128), (64, 8500, 384),
@@ -694,23 +661,21 @@ def test_bf16_device_api_many_splits(pmm):
 
 @pytest.mark.parametrize("whole", ["0", "1"])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-@pytest.mark.parametrize("kernel", ["wide", "ws"])
-def test_bf16_whole_block_runs(pmm, metric, whole, kernel, monkeypatch):
-    # M >= BM x grid query rows (BM = 128 for the default wave-specialised
-    # kernel, 256 for the opt-in wide one).  PMM_BF16_WHOLE=1 (default): the first 256 query
+def test_bf16_whole_block_runs(pmm, metric, whole, monkeypatch):
+    # M >= BM x grid query rows (BM = 128 for the wave-specialised kernel).
+    # PMM_BF16_WHOLE=1 (default): the first 256 query
     # blocks run whole (split by split, row state carried across splits), the
     # remaining 2-3 blocks as split units; 0: every unit a split unit.  Every
     # row vs float64 truth.
     import torch
 
     monkeypatch.setenv("PMM_BF16_WHOLE", whole)
-    monkeypatch.setenv("PMM_BF16_WIDE", "1" if kernel == "wide" else "0")
 
     n = _native()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(11)
-    m, N, d, k = (66000 if kernel == "wide" else 33000), 30000, 256, 50
+    m, N, d, k = 33000, 30000, 256, 50
     q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
     c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
     oi = torch.empty((m, k), dtype=torch.int32, device=dev)
@@ -831,3 +796,102 @@ def test_host_chunked_upload_equals_one_launch(pmm, metric, monkeypatch):
     oi, osc = oracle.topk(q[:40], c, 100, METRICS[metric])
     got = gpu_topk(q[:40], c, 100, metric)
     assert_bitexact(got[0], got[1], oi, osc, f"chunked {metric}")
+
+
+# ---- multi-GPU through the drop-in boundary (pmm_set_devices) ----
+# The box has one GPU: listing device 0 several times runs every shard on it
+# through the same code path as distinct GPUs (per-shard top-k with global
+# indices, peer copy of each [2][m][k] list into the root's gather buffer,
+# k-way merge there).  The result must equal the one-device result bit for bit.
+
+@pytest.fixture
+def device_list():
+    n = _native()
+    yield n
+    n.set_devices([])
+
+
+@pytest.mark.parametrize("shards", [2, 3, 8])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_set_devices_sharded_host_topk_bitexact(pmm, device_list, shards, metric):
+    n = device_list
+    rs = np.random.RandomState(shards * 7 + len(metric))
+    m, N, d, k = 300, 20011, 200, 100
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(N, d).astype(np.float32)
+    c[N - 40:] = c[:40]  # exact ties across shard boundaries
+    want = n.topk_host(q, c, k, METRICS[metric])
+    n.set_devices([0] * shards)
+    assert n.get_devices() == [0] * shards
+    got = n.topk_host(q, c, k, METRICS[metric])
+    assert np.array_equal(got[0], want[0]), float(np.mean(got[0] == want[0]))
+    assert np.array_equal(got[1].view(np.uint32), want[1].view(np.uint32))
+    oi, osc = oracle.topk(q, c, k, METRICS[metric])
+    assert_bitexact(got[0], got[1], oi, osc, f"set_devices x{shards} {metric}")
+
+
+def test_set_devices_shards_smaller_than_k(pmm, device_list):
+    # 8 shards of 12-13 rows with k = 64: every shard's list is padded with
+    # empty slots, which the merge skips
+    n = device_list
+    rs = np.random.RandomState(3)
+    q = rs.randn(40, 48).astype(np.float32)
+    c = rs.randn(100, 48).astype(np.float32)
+    want = n.topk_host(q, c, 64, METRICS["cosine"])
+    n.set_devices([0] * 8)
+    got = n.topk_host(q, c, 64, METRICS["cosine"])
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    n.set_devices([0] * 5)
+    got = n.topk_host(q, c[:3], 3, METRICS["cosine"])  # fewer rows than devices: 3 shards of one row
+    assert np.array_equal(got[0], n.topk_host(q, c[:3], 3, METRICS["cosine"])[0])
+
+
+def test_set_devices_bf16_compute(pmm, device_list):
+    n = device_list
+    rs = np.random.RandomState(9)
+    q = rs.randn(257, 384).astype(np.float32)
+    c = rs.randn(30000, 384).astype(np.float32)
+    want = n.topk_host(q, c, 50, METRICS["cosine"], compute=n.COMPUTE_BF16)
+    n.set_devices([0, 0, 0])
+    got = n.topk_host(q, c, 50, METRICS["cosine"], compute=n.COMPUTE_BF16)
+    # each shard is the exact top-k of the bf16 rows up to f32 accumulation
+    # order, checked against the truth of the rounded rows
+    _bf16_truth_check(q, c, 50, "cosine", got[0], got[1], "bf16 x3 devices")
+    assert float(np.mean(got[0] == want[0])) > 0.99
+
+
+def test_set_devices_sharded_corpus_handle(pmm, device_list):
+    # a corpus handle created under a device list is row-sharded at creation
+    # (per-device corpus cache); its searches equal the one-device handle's
+    n = device_list
+    rs = np.random.RandomState(21)
+    q = rs.randn(500, 256).astype(np.float32)
+    c = rs.randn(50000, 256).astype(np.float32)
+    one = n.DeviceCorpus(c)
+    assert one.shards == 1
+    n.set_devices([0, 0, 0, 0])
+    four = n.DeviceCorpus(c)
+    assert four.shards == 4
+    for metric in ("cosine", "euclidean", "dot"):
+        a = one.topk(q, 100, METRICS[metric])
+        b = four.topk(q, 100, METRICS[metric])
+        assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]), metric
+    one.close()
+    four.close()
+
+
+def test_set_devices_through_extension_and_cache(pmm, device_list):
+    from polars_matmul import _polars_matmul as pm
+
+    rs = np.random.RandomState(5)
+    q = rs.randn(64, 128).astype(np.float32)
+    c = rs.randn(9000, 128).astype(np.float32)
+    carr = pa.FixedSizeListArray.from_arrays(pa.array(c.reshape(-1)), 128)
+    qarr = pa.FixedSizeListArray.from_arrays(pa.array(q.reshape(-1)), 128)
+    want = pm._topk(qarr, carr, 10, "cosine").to_pylist()
+    pm.set_devices([0, 0])
+    try:
+        for _ in range(2):  # second call: the (sharded) cached handle
+            assert pm._topk(qarr, carr, 10, "cosine").to_pylist() == want
+    finally:
+        pm.clear_corpus_cache()

@@ -8,6 +8,15 @@ wave-specialised kernel spilled 592 B per lane into its MFMA loop and
 returned wrong scores (csrc/pmm_bf16_ws_kernel.h, Carve::SLOT_REPEATS).  This
 test compiles every instantiation to ISA and asserts that no basic block
 holding an MFMA holds scratch (spill) code.
+
+Scope: this guards ONE failure mode, spill/reload code next to the asm
+MFMAs.  It does not prove the general hazard rules: an ordinary
+compiler-scheduled VALU write to a register an in-flight asm MFMA reads, or a
+read of its accumulator too early, in the same block would pass.  The kernels
+keep such accesses out of the MFMA streams by construction (fragments are
+loaded by LDS reads the compiler waits for before the asm statement that
+names them; accumulators are read only after `mfma_drain`'s padding), and the
+GPU parity tests check the results.
 """
 import os
 import re
@@ -25,12 +34,11 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
 
 # (source, defines): every padded-D instantiation of the wave-specialised
 # kernel, the ring sizes whose slot sequence repeats per tile, and the
-# other two bf16 kernels at the largest D
+# one-wave-per-SIMD bf16 kernel at the largest D
 BUILDS = [("pmm_bf16_ws_ks.hip", [f"-DPMM_BF16_KS={k}"]) for k in range(1, 7)] + [
     ("pmm_bf16_ws_ks.hip", ["-DPMM_BF16_KS=6", "-DPMM_WS_NST=6"]),
     ("pmm_bf16_ws_ks.hip", ["-DPMM_BF16_KS=6", "-DPMM_WS_NST=3"]),
     ("pmm_bf16_ks.hip", ["-DPMM_BF16_KS=6"]),
-    ("pmm_bf16_wide_ks.hip", ["-DPMM_BF16_KS=6"]),
 ]
 
 _LABEL = re.compile(r"^(\.LBB\S*:|; %bb\.\d+:)")
