@@ -895,3 +895,66 @@ def test_set_devices_through_extension_and_cache(pmm, device_list):
             assert pm._topk(qarr, carr, 10, "cosine").to_pylist() == want
     finally:
         pm.clear_corpus_cache()
+
+
+# ---- the 256-row bf16 kernel (pmm_bf16_dsx_kernel.h; default at padded D
+# 256 / 512 / 768) against the wave-specialised kernel and float64 truth ----
+
+@pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (520, 40000, 768, 100), (70, 3000, 500, 192),
+                                     (257, 20011, 768, 448), (1, 1000, 256, 1), (600, 999, 700, 64)])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_dsx_kernel_vs_truth_and_ws(pmm, m, n, d, k, metric, monkeypatch):
+    # both kernels are the exact top-k of the bf16 rows up to f32 summation
+    # order (dsx: two K-half chains of 16x16x32 MFMAs added; ws: one chain of
+    # 32x32x16): each passes the truth check, and they agree but for near-ties
+    rs = np.random.RandomState(m + n + d + k + 7)
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    c[n // 2:n // 2 + 20] = c[:20]  # exact ties across the corpus
+    monkeypatch.setenv("PMM_BF16_DSX", "1")
+    di, ds = gpu_topk_bf16(q, c, k, metric)
+    _bf16_truth_check(q, c, k, metric, di, ds, f"bf16 dsx {m}x{n}x{d} k={k} {metric}")
+    monkeypatch.setenv("PMM_BF16_DSX", "0")
+    wi, ws_ = gpu_topk_bf16(q, c, k, metric)
+    assert float(np.mean(di == wi)) > 0.98
+    assert np.max(np.abs(ds.astype(np.float64) - ws_)) < 1e-4 * max(1.0, float(np.max(np.abs(ws_))))
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean", "dot"])
+def test_bf16_dsx_whole_blocks_and_splits(pmm, metric, monkeypatch):
+    # PMM_CUS=16: 129 query blocks of 256 rows on 16 workgroups, so 128 run
+    # whole (row state carried across 16+ splits) and one as split units;
+    # every row vs float64 truth on device
+    import torch
+
+    monkeypatch.setenv("PMM_CUS", "16")
+    n = _native()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(23)
+    m, N, d, k = 33000, 12000, 512, 40
+    q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
+    c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
+    oi = torch.empty((m, k), dtype=torch.int32, device=dev)
+    osc = torch.empty((m, k), dtype=torch.float32, device=dev)
+    n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS[metric],
+                       oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    qd, cd = q.double(), c.double()
+    if metric == "euclidean":
+        s = torch.cdist(qd, cd)
+        largest = False
+    else:
+        s = qd @ cd.T
+        if metric == "cosine":
+            s = s / (qd.norm(dim=1, keepdim=True) * cd.norm(dim=1)[None, :])
+        largest = True
+    ref_s, _ = torch.topk(s, k, dim=1, largest=largest)
+    got_true = torch.gather(s, 1, oi.long())
+    kth = ref_s[:, -1:]
+    tol = 1e-5 * kth.abs() + 1e-5 + (2e-6 * qd.norm(dim=1, keepdim=True) * cd.norm(dim=1).max() if metric == "dot" else 0)
+    ok = (got_true >= kth - tol) if largest else (got_true <= kth + tol)
+    assert bool(ok.all()), float(ok.float().mean())
+    assert float((osc.double() - got_true).abs().max()) < 1e-4 * max(1.0, float(ref_s.abs().max()))
+    srt = torch.sort(oi, dim=1).values
+    assert bool((srt[:, 1:] != srt[:, :-1]).all())
