@@ -121,6 +121,17 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
  * out (m x n, row-major) = Q * C^T. */
 int pmm_matmul_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d, float *out);
 
+/* Page-locked host memory for results (hipHostMalloc, portable to every
+ * device).  `.pmm.matmul` returns an m x n matrix (40 MB at the reference
+ * benchmark's size): written into a fresh pageable buffer, the call pays that
+ * buffer's page faults and the runtime's staging; into a page-locked one the
+ * D2H copy runs at link rate.  The Python layer keeps a pool of these and
+ * hands them to Arrow as foreign buffers (the reference moves its result Vec
+ * into the Series the same way, src/matmul.rs:116-124).  No reference
+ * counterpart of the allocation itself. */
+int pmm_host_alloc(size_t bytes, void **out);
+int pmm_host_free(void *p);
+
 /* Replaces matmul_slice_f64 / matmul_f64 (src/metrics.rs:111-157, :40-97). */
 int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t d,
                    double *out);

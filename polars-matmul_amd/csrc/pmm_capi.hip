@@ -403,6 +403,10 @@ struct HostPin {
   void *p = nullptr;
   HostPin(void *ptr, size_t bytes) {
     static const bool on = !(getenv("PMM_PIN_OUTPUT") && atoi(getenv("PMM_PIN_OUTPUT")) == 0);
+    // already page-locked (pmm_host_alloc's buffers, or the caller's): nothing to do
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, ptr) == hipSuccess && at.type == hipMemoryTypeHost) return;
+    (void)hipGetLastError();
     if (on && bytes >= (size_t(8) << 20) && hipHostRegister(ptr, bytes, hipHostRegisterDefault) == hipSuccess)
       p = ptr;
     else
@@ -1231,6 +1235,19 @@ int pmm_set_device(int device) {
   if (device < 0 || device >= n) return fail(PMM_ERR_NODEVICE, "no HIP device %d (%d visible)", device, n);
   HIP_TRY(hipSetDevice(device));
   t_ctx.device = device;
+  return PMM_OK;
+}
+
+int pmm_host_alloc(size_t bytes, void **out) {
+  if (!out) return fail(PMM_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (bytes == 0) return PMM_OK;
+  HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocPortable));
+  return PMM_OK;
+}
+
+int pmm_host_free(void *p) {
+  if (p) HIP_TRY(hipHostFree(p));
   return PMM_OK;
 }
 

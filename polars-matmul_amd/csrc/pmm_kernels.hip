@@ -565,24 +565,47 @@ hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid
 //             composite, so everything below it is dropped on load.
 //   loader 1: gathered per-shard (idx, score) lists [M][S][k_in] (multi-GPU).
 // ===========================================================================
+// The merge scratch is padded by one u64 every 32 (MP): a 32-lane group of
+// ds_read_b64 / ds_write_b64 then covers 64 distinct banks for the strided
+// bitonic partners and the compacted appends (unpadded, every such access
+// was 2-way conflicted: one conflict cycle per LDS instruction at c3).
+#define MP(i) ((i) + ((i) >> 5))
+__device__ inline void wave_sort_desc_u64_pad(u64 *s, int P, int lane) {
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = lane; i < (P >> 1); i += 64) {
+        const int x0 = ((i & ~(stride - 1)) << 1) | (i & (stride - 1));
+        const int x1 = x0 + stride;
+        const u64 a = s[MP(x0)], b = s[MP(x1)];
+        const bool desc = (x0 & size) == 0;
+        if (desc ? (a < b) : (a > b)) {
+          s[MP(x0)] = b;
+          s[MP(x1)] = a;
+        }
+      }
+      wave_sync();
+    }
+  }
+}
+
 __device__ int merge_compact(u64 *scr, int cnt, int k, int P, u64 *T, int lane) {
   if (P <= 512 && cnt > k) {
     // select the k best (wave_kth_u64), keep them unordered
     u64 x[8];
 #pragma unroll
-    for (int e = 0; e < 8; e++) x[e] = (lane + 64 * e < cnt) ? scr[lane + 64 * e] : 0ull;
+    for (int e = 0; e < 8; e++) x[e] = (lane + 64 * e < cnt) ? scr[MP(lane + 64 * e)] : 0ull;
     wave_sync();  // every lane has read before any rewrites
     const u64 t = wave_kth_u64<8>(x, k);
     if (t > *T) *T = t;
-    cnt = wave_keep_ge<8>(x, t, [&](int pos, u64 v) __attribute__((always_inline)) { scr[pos] = v; }, lane);
+    cnt = wave_keep_ge<8>(x, t, [&](int pos, u64 v) __attribute__((always_inline)) { scr[MP(pos)] = v; }, lane);
     wave_sync();
     return cnt;
   }
-  for (int i = cnt + lane; i < P; i += 64) scr[i] = 0ull;
+  for (int i = cnt + lane; i < P; i += 64) scr[MP(i)] = 0ull;
   wave_sync();
-  wave_sort_desc_u64(scr, P, lane);
+  wave_sort_desc_u64_pad(scr, P, lane);
   if (cnt >= k) {
-    const u64 t = scr[k - 1];
+    const u64 t = scr[MP(k - 1)];
     if (t > *T) *T = t;
     cnt = k;
   }
@@ -597,7 +620,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int row = blockIdx.x * wpb + wid;
   if (row >= a.M) return;  // whole wave exits; no block-wide barriers below
-  u64 *scr = (u64 *)smem + (size_t)wid * a.P;
+  u64 *scr = (u64 *)smem + (size_t)wid * MP(a.P);
   u64 T = (LOADER == 0) ? a.gthr[row] : 0ull;
   int cnt = 0;
   // candidate i of list s as a composite key (0 = empty)
@@ -613,7 +636,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     const bool keep = (x != 0ull) && (x >= T);
     const u64 m = __ballot(keep);
     const int pos = cnt + lanes_below(m);
-    if (keep) scr[pos] = x;
+    if (keep) scr[MP(pos)] = x;
     cnt += __popcll(m);
     if (cnt > a.P - 64) {
       wave_sync();
@@ -669,12 +692,12 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   if (PMM_ABL(a.ablate) != 1) {
     if (cnt > a.k_out && a.P <= 512) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
     const int P2 = min(a.P, next_pow2_dev(cnt));
-    for (int i = cnt + lane; i < P2; i += 64) scr[i] = 0ull;
+    for (int i = cnt + lane; i < P2; i += 64) scr[MP(i)] = 0ull;
     wave_sync();
-    wave_sort_desc_u64(scr, P2, lane);
+    wave_sort_desc_u64_pad(scr, P2, lane);
   }
   for (int j = lane; j < a.k_out; j += 64) {
-    const u64 x = (j < cnt) ? scr[j] : 0ull;
+    const u64 x = (j < cnt) ? scr[MP(j)] : 0ull;
     uint32_t id = 0xFFFFFFFFu;
     float sc = __uint_as_float(0x7FC00000u);
     if (x != 0ull) {
@@ -689,7 +712,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   }
 }
 
-size_t merge_lds_bytes_per_wave(int P) { return (size_t)P * 8; }
+size_t merge_lds_bytes_per_wave(int P) { return (size_t)MP(P) * 8; }
 
 // ===========================================================================
 // Threshold seeding (topk_f32_device_impl): one wave per query row reads the
@@ -956,6 +979,15 @@ hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s) {
   wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
   const size_t lds = (size_t)wpb * merge_lds_bytes_per_wave(a.P);
   const unsigned grid = (unsigned)((a.M + wpb - 1) / wpb);
+  if (lds > 65536) {  // (P = 8192 with the padding: 66 KiB)
+    static bool attr_set[2] = {false, false};
+    if (!attr_set[loader]) {
+      const void *fn = loader == 0 ? (const void *)merge_kernel<0> : (const void *)merge_kernel<1>;
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+      attr_set[loader] = true;
+    }
+  }
   if (loader == 0) merge_kernel<0><<<grid, wpb * 64, lds, s>>>(a);
   else merge_kernel<1><<<grid, wpb * 64, lds, s>>>(a);
   return hipGetLastError();

@@ -52,6 +52,8 @@ EXPORTED_SYMBOLS = (
     "pmm_topk_f64",
     "pmm_matmul_f32",
     "pmm_matmul_f64",
+    "pmm_host_alloc",
+    "pmm_host_free",
     "pmm_topk_workspace_bytes",
     "pmm_topk_merge_bytes",
     "pmm_topk_f32_device",
@@ -122,6 +124,8 @@ _SIGS = {
     "pmm_topk_f64": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_matmul_f32": ([_vp, _i64, _vp, _i64, _i64, _vp], _i32),
     "pmm_matmul_f64": ([_vp, _i64, _vp, _i64, _i64, _vp], _i32),
+    "pmm_host_alloc": ([_sz, ctypes.POINTER(ctypes.c_void_p)], _i32),
+    "pmm_host_free": ([_vp], _i32),
     "pmm_topk_workspace_bytes": ([_i64, _i64, _i64, _i64, _i32, _i32], _sz),
     "pmm_topk_merge_bytes": ([_vp, _i64, _i64, _i64, _i64, _i32, _i32, ctypes.POINTER(ctypes.c_uint64)], _i32),
     "pmm_topk_f32_device": (
@@ -238,10 +242,92 @@ def topk_host(q: np.ndarray, c: np.ndarray, k: int, metric: int, compute: int = 
     return idx, sc
 
 
+class _PinnedBlock:
+    """One page-locked host block of the result pool; returns itself to the
+    pool when the last array / Arrow buffer viewing it is released."""
+
+    __slots__ = ("ptr", "nbytes", "pool", "__weakref__")
+
+    def __init__(self, ptr_value: int, nbytes: int, pool: "PinnedPool"):
+        self.ptr, self.nbytes, self.pool = ptr_value, nbytes, pool
+
+    def __del__(self):  # pragma: no cover - exercised through the GC
+        try:
+            self.pool._give_back(self.ptr, self.nbytes)
+        except Exception:
+            pass
+
+
+class PinnedPool:
+    """Recycled page-locked result buffers (pmm_host_alloc).  A `.pmm.matmul`
+    result (m x n values) lands in one of these: no page faults, D2H at link
+    rate, and the buffer becomes the Arrow child buffer of the result Series
+    without a copy.  Blocks come back when their arrays are freed; at most
+    `cap_bytes` of idle blocks are kept (PMM_PINNED_POOL_BYTES, default 1 GiB;
+    0 disables the pool)."""
+
+    MIN_BYTES = 1 << 20  # smaller results: a plain numpy array
+
+    def __init__(self, cap_bytes: int):
+        self.cap = cap_bytes
+        self.free = {}  # nbytes -> [ptr, ...]
+        self.idle = 0
+        self.lock = threading.Lock()
+
+    def take(self, nbytes: int):
+        """A (pointer, owner) for nbytes, or None (pool off, too small, or the
+        allocation failed)."""
+        if self.cap <= 0 or nbytes < self.MIN_BYTES:
+            return None
+        with self.lock:
+            lst = self.free.get(nbytes)
+            if lst:
+                self.idle -= nbytes
+                p = lst.pop()
+                return p, _PinnedBlock(p, nbytes, self)
+        out = ctypes.c_void_p()
+        if _lib.pmm_host_alloc(nbytes, ctypes.byref(out)) != PMM_OK or not out.value:
+            return None
+        return out.value, _PinnedBlock(out.value, nbytes, self)
+
+    def _give_back(self, p: int, nbytes: int) -> None:
+        with self.lock:
+            if self.idle + nbytes <= self.cap:
+                self.free.setdefault(nbytes, []).append(p)
+                self.idle += nbytes
+                return
+        _lib.pmm_host_free(p)
+
+    def clear(self) -> None:
+        with self.lock:
+            ptrs = [p for lst in self.free.values() for p in lst]
+            self.free.clear()
+            self.idle = 0
+        for p in ptrs:
+            _lib.pmm_host_free(p)
+
+
+pinned_pool = PinnedPool(int(os.environ.get("PMM_PINNED_POOL_BYTES", str(1 << 30))))
+
+
+def pinned_empty(shape, dtype) -> np.ndarray:
+    """np.empty in a pooled page-locked block when one is available (the block
+    is owned by the returned array's buffer chain), else np.empty."""
+    dtype = np.dtype(dtype)
+    nbytes = int(np.prod(shape)) * dtype.itemsize
+    got = pinned_pool.take(nbytes)
+    if got is None:
+        return np.empty(shape, dtype=dtype)
+    p, owner = got
+    raw = (ctypes.c_char * nbytes).from_address(p)
+    raw._pmm_block = owner  # the array's base holds the block until released
+    return np.frombuffer(raw, dtype=dtype).reshape(shape)
+
+
 def matmul_host(q: np.ndarray, c: np.ndarray) -> np.ndarray:
     m, d = q.shape
     n = c.shape[0]
-    out = np.empty((m, n), dtype=q.dtype)
+    out = pinned_empty((m, n), q.dtype)
     fn = _lib.pmm_matmul_f32 if q.dtype == np.float32 else _lib.pmm_matmul_f64
     check(fn(ptr(q), m, ptr(c), n, d, ptr(out)))
     return out

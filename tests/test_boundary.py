@@ -339,3 +339,48 @@ def test_device_list_parse_and_validation():
         _native.set_devices([_native.device_count() + 5])
     assert ei.value.code == _native.PMM_ERR_NODEVICE
     assert _native.get_devices() == []
+
+
+def test_pinned_pool_recycles_blocks_and_falls_back(monkeypatch):
+    # .pmm.matmul results land in recycled page-locked
+    # blocks (no page faults, D2H at link rate); a block returns to the pool
+    # when its array (or the Arrow buffer viewing it) is freed.  The
+    # allocator is stubbed here (no HIP runtime work on CPU).
+    import gc
+
+    store = {}
+    frees = []
+
+    class StubLib:
+        def pmm_host_alloc(self, nbytes, out):
+            b = ctypes.create_string_buffer(nbytes)
+            store[ctypes.addressof(b)] = b
+            out._obj.value = ctypes.addressof(b)
+            return 0
+
+        def pmm_host_free(self, p):
+            frees.append(p)
+            return 0
+
+    monkeypatch.setattr(_native, "_lib", StubLib())
+    pool = _native.PinnedPool(64 << 20)
+    monkeypatch.setattr(_native, "pinned_pool", pool)
+    a = _native.pinned_empty((1024, 1024), np.float32)  # 4 MiB: pooled
+    assert a.flags.writeable and a.shape == (1024, 1024)
+    a[:] = 3.0
+    arr = pa.array(a.reshape(-1))  # Arrow view keeps the block alive
+    p = a.ctypes.data
+    del a
+    gc.collect()
+    assert pool.idle == 0 and float(arr[5].as_py()) == 3.0
+    del arr
+    gc.collect()
+    assert pool.idle == 4 << 20  # back in the pool
+    b = _native.pinned_empty((1024, 1024), np.float32)
+    assert b.ctypes.data == p and pool.idle == 0  # recycled, not reallocated
+    small = _native.pinned_empty((4, 4), np.float32)  # below MIN_BYTES: plain numpy
+    assert small.base is None or not hasattr(small.base, "_pmm_block")
+    del b
+    gc.collect()
+    pool.clear()
+    assert frees == [p]
