@@ -383,7 +383,20 @@ def kernel_stats(bf16):
     for key, nm in names.items():
         ms, n = _native.timing_read(nm)
         out[key] = (ms / n if n else None, n)
+    if bf16:
+        # which bf16 kernel ran (the library's timer names carry it)
+        out["bf16_kernel"] = next((v for v in ("dsx", "ws", "one-wave")
+                                   if _native.timing_read("gemm_bf16_topk/" + v)[1]), "ws")
     return out
+
+
+BF16_KERNEL_NAMES = {
+    "dsx": "gemm_bf16_dsx_kernel (256 query rows, K split over wave pairs: fused GEMM + metric + "
+           "top-k; + seed_bf16_dsx_kernel in achieved)",
+    "ws": "gemm_bf16_ws_kernel (wave-specialised fused GEMM + metric + top-k; "
+          "+ seed_bf16_ws_kernel in achieved)",
+    "one-wave": "gemm_bf16_kernel (one-wave fused GEMM + metric + top-k)",
+}
 
 
 def spot_check(q, c, lo, k, metric, out_i, out_s, rows, dist, world, rank):
@@ -465,8 +478,7 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8):
     ach = flops / (all_gemm_ms / 1000.0) / 1e12 if gemm_ms else None
     roof = {
         "bound": "mfma",
-        "kernel": ("gemm_bf16_ws_kernel (wave-specialised fused GEMM + metric + top-k; "
-                   "+ seed_bf16_ws_kernel in achieved)" if bf16 else
+        "kernel": (BF16_KERNEL_NAMES[ks["bf16_kernel"]] if bf16 else
                    "gemm_f32_kernel (fused GEMM + metric + top-k)"),
         "achieved": round(ach, 2) if ach else None,
         "peak": peak, "unit": "TFLOP/s",

@@ -54,6 +54,11 @@
 
 namespace pmm {
 
+#if !defined(PMM_LAB) || !defined(PMM_DSX_ABL)
+#undef PMM_DSX_ABL
+#define PMM_DSX_ABL 0
+#endif
+
 namespace dsx {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
@@ -292,6 +297,11 @@ __global__ __launch_bounds__(dsx::NTH, 1) void gemm_bf16_dsx_kernel(GemmF32Args 
   };
 
   bool sync_on = a.round_sync != 0;
+  // lab builds only (`make lab LAB=-DPMM_DSX_ABL=n`, results wrong; a
+  // compile-time constant: a runtime flag changes the register allocation):
+  // 1 = no epilogue, 2 = no corpus DMA, 4 = no MFMAs (fragment reads stay),
+  // 8 = no fragment reads
+  constexpr int abl = PMM_DSX_ABL;
   bf16x8 af[4][G2];  // the pair's 64 rows x this wave's K half: kept across a run's units
   for (int round = 0;; round++) {
     UnitPos u;
@@ -346,6 +356,7 @@ __global__ __launch_bounds__(dsx::NTH, 1) void gemm_bf16_dsx_kernel(GemmF32Args 
       const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.cb + (int64_t)col0 * a.ldc, (int64_t)nrow * a.ldc * 2);
       const int slot = (tile - t0) % NT;
       const uint32_t st = ring_lds + (uint32_t)(slot * STAGE);
+      if (abl & 2) return;
 #pragma unroll
       for (int i = 0; i < PW; i++)
         dma_b128(rb, __builtin_amdgcn_readfirstlane(st + (uint32_t)((i * NW + wid) * 1024)), b_voff(i));
@@ -424,6 +435,7 @@ __global__ __launch_bounds__(dsx::NTH, 1) void gemm_bf16_dsx_kernel(GemmF32Args 
     const uint32_t e_part_lds = smem_lds + OFF_E + (wid ^ 1) * EW + 2 * kh * 1024;
     const uint32_t cvr_lds = smem_lds + OFF_CVR;
     auto epilogue = [&](int pt) __attribute__((always_inline)) {
+      if (abl & 1) return;
       const int lane = lane_id(), c16 = lane & 15, q4 = lane >> 4;
       const uint32_t lo16 = (uint32_t)lane * 16u;
       f32x4 f0 = lds_ld128(e_part_lds + lo16);
@@ -494,6 +506,7 @@ __global__ __launch_bounds__(dsx::NTH, 1) void gemm_bf16_dsx_kernel(GemmF32Args 
       return (uint32_t)(((tile - t0) % NT) * STAGE) + frag_lane() + (uint32_t)(kh * G2 * 64);
     };
     auto rdfrag = [&](uint32_t fb, int j, int set) __attribute__((always_inline)) {
+      if (abl & 8) return;
       // kh G2 is a multiple of 4: substep j's XOR is (j & 3), its block j >> 2
       const uint32_t ad = ring_lds + ((fb ^ (uint32_t)(64 * (j & 3))) + (uint32_t)(256 * (j >> 2)));
       asm volatile("ds_read_b128 %0, %1" : "=v"(bq[set]) : "v"(ad) : "memory");
@@ -519,6 +532,7 @@ __global__ __launch_bounds__(dsx::NTH, 1) void gemm_bf16_dsx_kernel(GemmF32Args 
         // fragment j landed: the reads younger than it (LDS returns in
         // order) may stay in flight; the wait is tied to the fragment
         wait_frag(j, bq[j % (PF + 1)]);
+        if (!(abl & 4))
 #pragma unroll
         for (int rb = 0; rb < 4; rb++)
           acc[rb] = mfma(af[rb][j], bq[j % (PF + 1)], j == 0 ? (f32x4){0.f, 0.f, 0.f, 0.f} : acc[rb]);

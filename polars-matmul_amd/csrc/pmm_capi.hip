@@ -789,7 +789,8 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
       }
     }
     {
-      Timed t("gemm_bf16_topk", s);
+      // (the suffix names the kernel; pmm_timing_read matches substrings)
+      Timed t(p.variant == -4 ? "gemm_bf16_topk/dsx" : p.variant == -2 ? "gemm_bf16_topk/ws" : "gemm_bf16_topk/one-wave", s);
       HIP_TRY(p.variant == -4   ? launch_gemm_bf16_dsx(a, p.grid, s)
               : p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s)
                                 : launch_gemm_bf16(a, p.grid, s));
