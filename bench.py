@@ -342,7 +342,9 @@ def make_inputs(name, rank, world, dev):
     return q, c, lo, hi - lo
 
 
-def timed_steps(runner, steps, warmup, dist):
+def timed_steps(runner, steps, warmup, dist, stride=1):
+    """K timed steps; the library's per-kernel HIP events are recorded on
+    every `stride`-th step of the timed region (1 = every step)."""
     import torch
     from polars_matmul import _native
 
@@ -353,10 +355,13 @@ def timed_steps(runner, steps, warmup, dist):
         dist.barrier()
     torch.cuda.synchronize()
     _native.timing_reset()
-    _native.timing_enable(True)
     t0 = time.perf_counter()
     out = None
     for i in range(steps):
+        if stride > 1:
+            _native.timing_enable(i % stride == 0)
+        elif i == 0:
+            _native.timing_enable(True)
         out = runner.run()
         if steps <= 50:
             log(f"step {i + 1}/{steps} issued")
@@ -447,7 +452,7 @@ def spot_check(q, c, lo, k, metric, out_i, out_s, rows, dist, world, rank):
     }
 
 
-def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8):
+def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8, stride=1):
     """One config's timed line (inputs resident, K steps bracketed by barrier
     + synchronize, max over ranks).  Returns (fields, q, corpus shard)."""
     import torch
@@ -462,7 +467,7 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8):
     ws = torch.empty(_native.workspace_bytes(M, n_loc, D, k, mid, compute), dtype=torch.uint8, device=dev)
     runner = ShardedTopK(q, c, lo, k, mid, workspace=ws)
     torch.cuda.synchronize()
-    elapsed, (out_i, out_s) = timed_steps(runner, steps, warmup, dist)
+    elapsed, (out_i, out_s) = timed_steps(runner, steps, warmup, dist, stride)
     ks = kernel_stats(bf16)
     merge_bytes = _native.merge_bytes(ws.data_ptr(), M, n_loc, D, k, mid, compute) if ks["merge"][1] else None
     check = None
@@ -574,7 +579,7 @@ def extra_line(name, steps, warmup, dev, args):
     M, N, D = CONFIGS[name][:3]
     small = M * N * D < 10**11  # sub-millisecond steps: time more of them
     st, wu = (max(steps, 200), max(warmup, 10)) if small else (steps, warmup)
-    fields, q, c, lists = measure(name, st, wu, 0, 1, None, dev, check_rows=8)
+    fields, q, c, lists = measure(name, st, wu, 0, 1, None, dev, check_rows=8, stride=args.timing_stride)
     ref = args.ref_lists.get(CONFIGS[name][:5])
     if CONFIGS[name][5] == "bf16" and ref is not None and fields["check"] is not None:
         # SURVEY 8c's bf16 bar: recall@k of the bf16 lists against the f32
@@ -621,6 +626,8 @@ def main():
                     help="comma-separated secondary configs measured after the main line (N=1; 'none' = none; "
                          "'matmul' = .pmm.matmul at the c1 size)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 top-k")
+    ap.add_argument("--timing-stride", type=int, default=1,
+                    help="record the per-kernel HIP events on every n-th timed step")
     ap.add_argument("--cpu-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -656,7 +663,8 @@ def main():
     _native.check(_native.lib().pmm_set_device(torch.cuda.current_device()))
 
     M, N, D, k, metric, cdt = CONFIGS[args.config]
-    fields, q, c, lists = measure(args.config, args.steps, args.warmup, rank, world, dist, dev, args.check)
+    fields, q, c, lists = measure(args.config, args.steps, args.warmup, rank, world, dist, dev, args.check,
+                                  args.timing_stride)
     if fields["check"]:
         log(f"spot check: {fields['check']}")
     # f32 lists of this workload's (M, N, D, k, metric) for the bf16 recall check of an extra line

@@ -54,6 +54,9 @@
 
 namespace pmm {
 
+#ifndef PMM_DSX_SEL
+#define PMM_DSX_SEL 1  // survivor values selected from registers, not re-read from LDS
+#endif
 #if !defined(PMM_LAB) || !defined(PMM_DSX_ABL)
 #undef PMM_DSX_ABL
 #define PMM_DSX_ABL 0
@@ -300,7 +303,7 @@ __global__ __launch_bounds__(dsx::NTH, 1) void gemm_bf16_dsx_kernel(GemmF32Args 
   // lab builds only (`make lab LAB=-DPMM_DSX_ABL=n`, results wrong; a
   // compile-time constant: a runtime flag changes the register allocation):
   // 1 = no epilogue, 2 = no corpus DMA, 4 = no MFMAs (fragment reads stay),
-  // 8 = no fragment reads
+  // 8 = no fragment reads, 16 = pre-filter only (no survivors queued)
   constexpr int abl = PMM_DSX_ABL;
   bf16x8 af[4][G2];  // the pair's 64 rows x this wave's K half: kept across a run's units
   for (int round = 0;; round++) {
@@ -460,10 +463,12 @@ __global__ __launch_bounds__(dsx::NTH, 1) void gemm_bf16_dsx_kernel(GemmF32Args 
 #pragma unroll
       for (int i = 0; i < 4; i++) bits = (bits << 1) | (uint32_t)!(prefilter_diff<METRIC>(f1[i], cv, l1[i]) < 0.0f);
       if (gcol >= a.N) bits = 0u;
-      if (__ballot(bits != 0u) == 0ull) return;
+      if (__ballot(bits != 0u) == 0ull || (abl & 16)) return;
+#if !PMM_DSX_SEL
       lds_st128(e_own_lds + lo16, f0);
       lds_st128(e_own_lds + 1024 + lo16, f1);
       wait_lgkm0();
+#endif
       for (;;) {
         const bool act = bits != 0u;
         const u64 mk = __ballot(act);
@@ -472,8 +477,16 @@ __global__ __launch_bounds__(dsx::NTH, 1) void gemm_bf16_dsx_kernel(GemmF32Args 
           const int j = 31 - __builtin_clz(bits);  // bit j <-> e = 7 - j
           bits &= ~(1u << j);
           const int e = 7 - j;
+#if PMM_DSX_SEL
+          // the value by selects over the finals (no LDS round trip)
+          const float s01 = (e & 1) ? f0[1] : f0[0], s23 = (e & 1) ? f0[3] : f0[2];
+          const float s45 = (e & 1) ? f1[1] : f1[0], s67 = (e & 1) ? f1[3] : f1[2];
+          const float slo = (e & 2) ? s23 : s01, shi = (e & 2) ? s67 : s45;
+          const uint32_t v = __float_as_uint((e & 4) ? shi : slo);
+#else
           uint32_t v = lds_ld32(e_own_lds + (uint32_t)((e >> 2) * 1024 + (e & 3) * 4) + lo16);
           ready(v);
+#endif
           const uint32_t rl = (uint32_t)((e >> 2) * 16 + q4 * 4 + (e & 3));
           const u64 item = (u64)v | ((u64)(rl | ((uint32_t)gcol << 5)) << 32);
           lds_st64(lq_lds + (uint32_t)(qlen + lanes_below(mk)) * 8u, item);

@@ -66,6 +66,7 @@ std::vector<int> g_devs;
 struct TimingRec {
   const char *name;
   hipEvent_t a, b;
+  int dev;
 };
 
 // Per-thread, per-device scratch arena.  Host entry points use it on the
@@ -89,8 +90,24 @@ struct ThreadCtx {
   std::vector<ArenaSlot> arena;      // per device
   bool timing = false;
   std::vector<TimingRec> recs;
+  // events of read timing records, per device, reused (an event creation per
+  // timed launch is host time comparable to a small problem's whole step)
+  std::vector<std::vector<hipEvent_t>> free_events;
 };
 thread_local ThreadCtx t_ctx;
+
+hipEvent_t timing_event(int dev) {
+  if ((int)t_ctx.free_events.size() <= dev) t_ctx.free_events.resize(dev + 1);
+  auto &v = t_ctx.free_events[dev];
+  hipEvent_t e = nullptr;
+  if (!v.empty()) {
+    e = v.back();
+    v.pop_back();
+  } else {
+    (void)hipEventCreate(&e);
+  }
+  return e;
+}
 
 // Restores the caller's current HIP device when a host entry point switched it.
 struct DevScope {
@@ -194,8 +211,9 @@ struct Timed {
   Timed(const char *name, hipStream_t st) : s(st), on(t_ctx.timing) {
     if (on) {
       rec.name = name;
-      (void)hipEventCreate(&rec.a);
-      (void)hipEventCreate(&rec.b);
+      (void)hipGetDevice(&rec.dev);
+      rec.a = timing_event(rec.dev);
+      rec.b = timing_event(rec.dev);
       (void)hipEventRecord(rec.a, s);
     }
   }
@@ -287,8 +305,10 @@ bool bf16_ws_enabled(int capg, int64_t d) {
 // applies (padded D of 256, 512 or 768; capg <= kBf16WsMaxCapg).
 // PMM_BF16_DSX=0 falls back to the wave-specialised kernel.  Read per call.
 bool bf16_dsx_enabled(int capg, int64_t d) {
+  // opt-in (PMM_BF16_DSX=1): measured slower than the wave-specialised
+  // kernel at c4
   const char *e = getenv("PMM_BF16_DSX");
-  if (e && atoi(e) == 0) return false;
+  if (!e || atoi(e) == 0) return false;
   const int dp = (int)(cdiv(d, kBf16DAlign) * kBf16DAlign);
   return capg <= kBf16WsMaxCapg && bf16_dsx_supported(dp) && gemm_bf16_dsx_lds_bytes(dp) <= 160 * 1024;
 }
@@ -1797,8 +1817,10 @@ int pmm_timing_enable(int enable) {
 
 int pmm_timing_reset(void) {
   for (auto &r : t_ctx.recs) {
-    (void)hipEventDestroy(r.a);
-    (void)hipEventDestroy(r.b);
+    (void)hipEventSynchronize(r.b);
+    if ((int)t_ctx.free_events.size() <= r.dev) t_ctx.free_events.resize(r.dev + 1);
+    t_ctx.free_events[r.dev].push_back(r.a);
+    t_ctx.free_events[r.dev].push_back(r.b);
   }
   t_ctx.recs.clear();
   return PMM_OK;

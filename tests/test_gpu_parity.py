@@ -897,8 +897,9 @@ def test_set_devices_through_extension_and_cache(pmm, device_list):
         pm.clear_corpus_cache()
 
 
-# ---- the 256-row bf16 kernel (pmm_bf16_dsx_kernel.h; default at padded D
-# 256 / 512 / 768) against the wave-specialised kernel and float64 truth ----
+# ---- the 256-row bf16 kernel (pmm_bf16_dsx_kernel.h; opt-in by PMM_BF16_DSX=1
+# at padded D 256 / 512 / 768) against the wave-specialised kernel and float64
+# truth ----
 
 @pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (520, 40000, 768, 100), (70, 3000, 500, 192),
                                      (257, 20011, 768, 448), (1, 1000, 256, 1), (600, 999, 700, 64)])
@@ -928,6 +929,7 @@ def test_bf16_dsx_whole_blocks_and_splits(pmm, metric, monkeypatch):
     import torch
 
     monkeypatch.setenv("PMM_CUS", "16")
+    monkeypatch.setenv("PMM_BF16_DSX", "1")
     n = _native()
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
