@@ -357,6 +357,11 @@ def timed_steps(runner, steps, warmup, dist, stride=1):
     _native.timing_reset()
     t0 = time.perf_counter()
     out = None
+    if stride <= 0:
+        # a sub-millisecond step: the events themselves (8 records per step)
+        # add ~20 us to it (c1 0.142 ms with them on every step, 0.119 on
+        # every 64th; profiles/r3_c1/timing_stride.txt), so they sample it
+        stride = 1 if steps <= 20 else 50
     for i in range(steps):
         if stride > 1:
             _native.timing_enable(i % stride == 0)
@@ -493,6 +498,7 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8, stride=1)
         # (small problems only) is its own launch of the same
         # kernel and is counted in "achieved"/"frac" too
         "kernel_ms_avg": round(gemm_ms, 3) if gemm_ms else None,
+        "kernel_launches_timed": ks["gemm"][1],
         "seed_ms_avg": round(seed_ms, 3) if seed_ms else None,
         "flops_per_launch": flops,
         # the whole step (norms, fills, seed, GEMM, merge, gather) against the peak
@@ -626,8 +632,9 @@ def main():
                     help="comma-separated secondary configs measured after the main line (N=1; 'none' = none; "
                          "'matmul' = .pmm.matmul at the c1 size)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 top-k")
-    ap.add_argument("--timing-stride", type=int, default=1,
-                    help="record the per-kernel HIP events on every n-th timed step")
+    ap.add_argument("--timing-stride", type=int, default=0,
+                    help="record the per-kernel HIP events on every n-th timed step (0: every step of "
+                         "a run of at most 20 steps, every 50th of a longer one)")
     ap.add_argument("--cpu-selftest", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 

@@ -23,6 +23,13 @@
 
 using namespace pmm;
 
+#ifndef PMM_LAB
+// The 256-row bf16 kernel is in the lab build only; these are never called
+// (bf16_dsx_enabled is false outside it).
+hipError_t pmm::launch_gemm_bf16_dsx(const GemmF32Args &, int, hipStream_t) { return hipErrorNotSupported; }
+hipError_t pmm::launch_seed_bf16_dsx(const GemmF32Args &, float *, int, hipStream_t) { return hipErrorNotSupported; }
+#endif
+
 namespace {
 
 constexpr const char *kVersion = "0.1.4+mi355x.r1";
@@ -301,16 +308,21 @@ bool bf16_ws_enabled(int capg, int64_t d) {
   return capg <= kBf16WsMaxCapg && gemm_bf16_ws_lds_bytes(capg, dp) <= 160 * 1024;
 }
 
-// 256-query-row bf16 kernel (pmm_bf16_dsx_kernel.h): the default where it
-// applies (padded D of 256, 512 or 768; capg <= kBf16WsMaxCapg).
-// PMM_BF16_DSX=0 falls back to the wave-specialised kernel.  Read per call.
+// 256-query-row bf16 kernel (pmm_bf16_dsx_kernel.h; padded D of 256, 512 or
+// 768, capg <= kBf16WsMaxCapg): lab build only, PMM_BF16_DSX=1 (read per
+// call).  Measured slower than the wave-specialised kernel at c4 (DESIGN.md
+// §3c), so the shipped library does not contain it.
 bool bf16_dsx_enabled(int capg, int64_t d) {
-  // opt-in (PMM_BF16_DSX=1): measured slower than the wave-specialised
-  // kernel at c4
+#ifdef PMM_LAB
   const char *e = getenv("PMM_BF16_DSX");
   if (!e || atoi(e) == 0) return false;
   const int dp = (int)(cdiv(d, kBf16DAlign) * kBf16DAlign);
   return capg <= kBf16WsMaxCapg && bf16_dsx_supported(dp) && gemm_bf16_dsx_lds_bytes(dp) <= 160 * 1024;
+#else
+  (void)capg;
+  (void)d;
+  return false;
+#endif
 }
 
 // compute = PMM_COMPUTE_F32: the f32 kernel (variant chosen by LDS fit);

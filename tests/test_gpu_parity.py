@@ -897,10 +897,14 @@ def test_set_devices_through_extension_and_cache(pmm, device_list):
         pm.clear_corpus_cache()
 
 
-# ---- the 256-row bf16 kernel (pmm_bf16_dsx_kernel.h; opt-in by PMM_BF16_DSX=1
-# at padded D 256 / 512 / 768) against the wave-specialised kernel and float64
-# truth ----
+# ---- the 256-row bf16 kernel (pmm_bf16_dsx_kernel.h; lab build only: `make
+# lab`, PMM_LIB=libpmm_lab.so, PMM_BF16_DSX=1, padded D 256 / 512 / 768)
+# against the wave-specialised kernel and float64 truth ----
+needs_lab = pytest.mark.skipif(not os.environ.get("PMM_LIB", "").startswith("libpmm_lab"),
+                               reason="the 256-row bf16 kernel is in the lab build only (PMM_LIB=libpmm_lab.so)")
 
+
+@needs_lab
 @pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (520, 40000, 768, 100), (70, 3000, 500, 192),
                                      (257, 20011, 768, 448), (1, 1000, 256, 1), (600, 999, 700, 64)])
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
@@ -921,6 +925,7 @@ def test_bf16_dsx_kernel_vs_truth_and_ws(pmm, m, n, d, k, metric, monkeypatch):
     assert np.max(np.abs(ds.astype(np.float64) - ws_)) < 1e-4 * max(1.0, float(np.max(np.abs(ws_))))
 
 
+@needs_lab
 @pytest.mark.parametrize("metric", ["cosine", "euclidean", "dot"])
 def test_bf16_dsx_whole_blocks_and_splits(pmm, metric, monkeypatch):
     # PMM_CUS=16: 129 query blocks of 256 rows on 16 workgroups, so 128 run

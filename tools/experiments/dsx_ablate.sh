@@ -1,4 +1,6 @@
 #!/bin/bash
+# (lab libraries built by: make -C polars-matmul_amd lab LAB="-DPMM_DSX_ABL=<n>" and renamed
+#  polars_matmul/libpmm_lab.so -> libpmm_lab_dsx<n>.so / libpmm_lab_sel0.so with LAB="-DPMM_DSX_SEL=0")
 # bf16 256-row kernel (dsx) diagnosis at c4: lab ablation builds (compile-time
 # PMM_DSX_ABL: 1 no epilogue, 2 no corpus DMA, 4 no MFMAs, 8 no fragment
 # reads), then the rocprofv3 passes of tools/profile.sh on the shipped build,

@@ -1,4 +1,6 @@
 #!/bin/bash
+# (lab libraries built by: make -C polars-matmul_amd lab LAB="-DPMM_DSX_ABL=<n>" and renamed
+#  polars_matmul/libpmm_lab.so -> libpmm_lab_dsx<n>.so / libpmm_lab_sel0.so with LAB="-DPMM_DSX_SEL=0")
 # dsx round 2: bf16 dsx tests on the register-select survivor path, then c4
 # alternated: ws (default), dsx (shipped), dsx with the LDS re-read (lab
 # sel0), dsx pre-filter only (lab abl16, results wrong).

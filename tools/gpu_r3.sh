@@ -13,4 +13,14 @@ rc=$?; echo "smoke rc=$rc"; tail -1 gpurun_out/r3_smoke.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py > gpurun_out/r3_bench.json 2> gpurun_out/r3_bench.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/r3_bench.json
-exit $rc
+
+[ $rc -eq 0 ] || exit $rc
+# rocprofv3 summaries of the shipped kernels at c3 and c4 (tools/profile.sh:
+# a kernel-trace pass, then one PMC group per pass)
+P="--steps 2 --warmup 1 --boundary 0 --extra none --cpu-sample 0 --check 0"
+bash tools/profile.sh r3c3 --config c3 $P || exit 11
+python tools/pmc_summary.py gpurun_out/prof_r3c3 gemm_f32_kernel > gpurun_out/prof_r3c3/summary.json || exit 12
+python tools/pmc_summary.py gpurun_out/prof_r3c3 merge_kernel > gpurun_out/prof_r3c3/summary_merge.json || exit 12
+bash tools/profile.sh r3c4 --config c4 $P || exit 13
+python tools/pmc_summary.py gpurun_out/prof_r3c4 gemm_bf16_ws > gpurun_out/prof_r3c4/summary.json || exit 14
+echo profiles ok
