@@ -565,11 +565,33 @@ hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid
 //             composite, so everything below it is dropped on load.
 //   loader 1: gathered per-shard (idx, score) lists [M][S][k_in] (multi-GPU).
 // ===========================================================================
-// The merge scratch is padded by one u64 every 32 (MP): a 32-lane group of
-// ds_read_b64 / ds_write_b64 then covers 64 distinct banks for the strided
-// bitonic partners and the compacted appends (unpadded, every such access
-// was 2-way conflicted: one conflict cycle per LDS instruction at c3).
+// Merge scratch layout (PMM_MERGE_SWZ; MP maps a slot to its LDS position,
+// MPN is the slots allocated per wave).  A ds_read_b64 / ds_write_b64 is
+// served in two 32-lane groups, conflict-free when a group's 32 slots are
+// distinct mod 32.  The bitonic partners of strides 1..16 hit slots e and
+// e + 32 in one group (2-way conflicts at every such step):
+//   0: plain slots (default);
+//   1: one u64 of padding every 32 slots (slot + slot / 32): fixes stride 1
+//      only;
+//   2: slots 32..63 of every 64 XOR 31 (bits 0-4 flipped when bit 5 is set):
+//      every bitonic step conflict-free, no extra LDS.
+// Measured at c3 (alternated, tools/experiments/merge_swz.sh): 0.378-0.381
+// ms plain, 0.427-0.428 padded, 0.443-0.445 swizzled; c1 equal.  The merge
+// is issue- and latency-bound: the index arithmetic costs more than the
+// conflict cycles it removes.
+#ifndef PMM_MERGE_SWZ
+#define PMM_MERGE_SWZ 0
+#endif
+#if PMM_MERGE_SWZ == 1
 #define MP(i) ((i) + ((i) >> 5))
+#define MPN(P) MP(P)
+#elif PMM_MERGE_SWZ == 2
+#define MP(i) ((i) ^ ((((i) >> 5) & 1) * 31))
+#define MPN(P) (P)
+#else
+#define MP(i) (i)
+#define MPN(P) (P)
+#endif
 __device__ inline void wave_sort_desc_u64_pad(u64 *s, int P, int lane) {
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -620,7 +642,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   const int wpb = blockDim.x >> 6;
   const int row = blockIdx.x * wpb + wid;
   if (row >= a.M) return;  // whole wave exits; no block-wide barriers below
-  u64 *scr = (u64 *)smem + (size_t)wid * MP(a.P);
+  u64 *scr = (u64 *)smem + (size_t)wid * MPN(a.P);
   u64 T = (LOADER == 0) ? a.gthr[row] : 0ull;
   int cnt = 0;
   // candidate i of list s as a composite key (0 = empty)
@@ -712,7 +734,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   }
 }
 
-size_t merge_lds_bytes_per_wave(int P) { return (size_t)MP(P) * 8; }
+size_t merge_lds_bytes_per_wave(int P) { return (size_t)MPN(P) * 8; }
 
 // ===========================================================================
 // Threshold seeding (topk_f32_device_impl): one wave per query row reads the
