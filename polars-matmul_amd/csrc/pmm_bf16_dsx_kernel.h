@@ -554,6 +554,9 @@ __global__ __launch_bounds__(dsx::NTH, 1) void gemm_bf16_dsx_kernel(GemmF32Args 
     };
     // end of a tile: the partial sums to E
     auto end_tile = [&]() __attribute__((always_inline)) {
+      // the last MFMAs' results -> the asm stores reading them: 4-pass XDL,
+      // 8 wait states (hipcc pads nothing in front of an asm statement)
+      asm volatile("s_nop 7" : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]));
       const uint32_t ad = e_mine + (uint32_t)lane_id() * 16;
 #pragma unroll
       for (int rb = 0; rb < 4; rb++) lds_st128(ad + rb * 1024, acc[rb]);

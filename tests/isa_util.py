@@ -1,0 +1,52 @@
+"""gfx950 ISA of the inline-asm kernels, compiled once per test session
+(hipcc cross-compiles here; no GPU).  Shared by tests/test_kernel_resources.py
+and tests/test_asm_hazards.py."""
+import functools
+import os
+import shutil
+import subprocess
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "polars-matmul_amd", "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
+         "--cuda-device-only", "-S"]
+
+# (source, defines): every padded-D instantiation of the wave-specialised
+# kernel, the ring sizes whose slot sequence repeats per tile, the
+# one-wave-per-SIMD bf16 kernel at the largest D, and the lab-only 256-row
+# kernel's three instantiations
+BUILDS = [("pmm_bf16_ws_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
+    ("pmm_bf16_ws_ks.hip", ("-DPMM_BF16_KS=6", "-DPMM_WS_NST=6")),
+    ("pmm_bf16_ws_ks.hip", ("-DPMM_BF16_KS=6", "-DPMM_WS_NST=3")),
+    ("pmm_bf16_ks.hip", ("-DPMM_BF16_KS=6",)),
+] + [("pmm_bf16_dsx_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in (2, 4, 6)]
+
+
+def have_hipcc():
+    return os.path.exists(HIPCC)
+
+
+@functools.lru_cache(maxsize=None)
+def all_isa():
+    """{(source, defines): assembly text} for every entry of BUILDS, compiled
+    in parallel."""
+    tmp = tempfile.mkdtemp(prefix="pmm_isa_")
+    try:
+        procs = []
+        for i, (src, defs) in enumerate(BUILDS):
+            out = os.path.join(tmp, f"b{i}.s")
+            cmd = [HIPCC, *FLAGS, *defs, "-I", CSRC, "-o", out, os.path.join(CSRC, src)]
+            procs.append((src, defs, out, subprocess.Popen(cmd, stdout=subprocess.PIPE,
+                                                           stderr=subprocess.STDOUT)))
+        res = {}
+        for src, defs, out, p in procs:
+            log = p.communicate(timeout=600)[0].decode(errors="replace")
+            if p.returncode != 0:
+                raise RuntimeError(f"{src} {defs}: {log[-2000:]}")
+            with open(out) as f:
+                res[(src, defs)] = f.read()
+        return res
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)

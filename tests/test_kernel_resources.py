@@ -9,37 +9,15 @@ returned wrong scores (csrc/pmm_bf16_ws_kernel.h, Carve::SLOT_REPEATS).  This
 test compiles every instantiation to ISA and asserts that no basic block
 holding an MFMA holds scratch (spill) code.
 
-Scope: this guards ONE failure mode, spill/reload code next to the asm
-MFMAs.  It does not prove the general hazard rules: an ordinary
-compiler-scheduled VALU write to a register an in-flight asm MFMA reads, or a
-read of its accumulator too early, in the same block would pass.  The kernels
-keep such accesses out of the MFMA streams by construction (fragments are
-loaded by LDS reads the compiler waits for before the asm statement that
-names them; accumulators are read only after `mfma_drain`'s padding), and the
-GPU parity tests check the results.
+Scope: this guards spill/reload code next to the asm MFMAs; the wait-state
+rules between asm statements and compiler code are checked on the same ISA
+by tests/test_asm_hazards.py.
 """
-import os
 import re
-import shutil
-import subprocess
-import tempfile
 
 import pytest
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-CSRC = os.path.join(ROOT, "polars-matmul_amd", "csrc")
-HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
-         "--cuda-device-only", "-S"]
-
-# (source, defines): every padded-D instantiation of the wave-specialised
-# kernel, the ring sizes whose slot sequence repeats per tile, and the
-# one-wave-per-SIMD bf16 kernel at the largest D
-BUILDS = [("pmm_bf16_ws_ks.hip", [f"-DPMM_BF16_KS={k}"]) for k in range(1, 7)] + [
-    ("pmm_bf16_ws_ks.hip", ["-DPMM_BF16_KS=6", "-DPMM_WS_NST=6"]),
-    ("pmm_bf16_ws_ks.hip", ["-DPMM_BF16_KS=6", "-DPMM_WS_NST=3"]),
-    ("pmm_bf16_ks.hip", ["-DPMM_BF16_KS=6"]),
-] + [("pmm_bf16_dsx_ks.hip", [f"-DPMM_BF16_KS={k}"]) for k in (2, 4, 6)]
+from isa_util import all_isa, have_hipcc
 
 _LABEL = re.compile(r"^(\.LBB\S*:|; %bb\.\d+:)")
 
@@ -91,32 +69,18 @@ def mfma_blocks_with_spills(asm: str):
     return bad
 
 
-@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
+@pytest.mark.skipif(not have_hipcc(), reason="hipcc not available")
 def test_no_spill_code_beside_inline_asm_mfmas():
-    tmp = tempfile.mkdtemp(prefix="pmm_isa_")
-    try:
-        procs = []
-        for i, (src, defs) in enumerate(BUILDS):
-            out = os.path.join(tmp, f"b{i}.s")
-            cmd = [HIPCC, *FLAGS, *defs, "-I", CSRC, "-o", out, os.path.join(CSRC, src)]
-            procs.append((src, defs, out, subprocess.Popen(cmd, stdout=subprocess.PIPE,
-                                                           stderr=subprocess.STDOUT)))
-        failures = []
-        for src, defs, out, p in procs:
-            log = p.communicate(timeout=600)[0].decode(errors="replace")
-            assert p.returncode == 0, f"{src} {defs}: {log[-2000:]}"
-            with open(out) as f:
-                asm = f.read()
-            assert "v_mfma" in asm, f"{src} {defs}: no MFMA in the ISA"
-            bad = mfma_blocks_with_spills(asm)
-            if bad:
-                failures.append(f"{src} {' '.join(defs)}: {bad[:4]}")
-            m0 = compiler_m0_uses(asm)
-            if m0:
-                failures.append(f"{src} {' '.join(defs)}: compiler M0 use {m0[:2]}")
-        assert not failures, "spill code in MFMA blocks / compiler M0 use:\n" + "\n".join(failures)
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
+    failures = []
+    for (src, defs), asm in all_isa().items():
+        assert "v_mfma" in asm, f"{src} {defs}: no MFMA in the ISA"
+        bad = mfma_blocks_with_spills(asm)
+        if bad:
+            failures.append(f"{src} {' '.join(defs)}: {bad[:4]}")
+        m0 = compiler_m0_uses(asm)
+        if m0:
+            failures.append(f"{src} {' '.join(defs)}: compiler M0 use {m0[:2]}")
+    assert not failures, "spill code in MFMA blocks / compiler M0 use:\n" + "\n".join(failures)
 
 
 def test_detector_flags_a_spill_in_an_mfma_block():
