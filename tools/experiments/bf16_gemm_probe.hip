@@ -31,7 +31,10 @@ constexpr int BM = 256, BN = 256, KST = 32;  // tile, K per stage
 constexpr int NSTG = D / KST;                // stages per tile (24)
 constexpr int NS = 4;                        // ring slots
 constexpr int STAGE = (BM + BN) * KST * 2;   // 32 KiB
-constexpr int GQ = 4, GC = 8;                // per-XCD group: 4 query blocks x 8 corpus tiles
+constexpr int GQ = 4, GC = 8;
+#ifndef PROBE_ABL
+#define PROBE_ABL 0  // 1: no DMA (stale LDS), 2: no fragment reads
+#endif                // per-XCD group: 4 query blocks x 8 corpus tiles
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, (int)bytes, 0x00020000);
@@ -69,7 +72,7 @@ __global__ __launch_bounds__(256, 1) void probe(Args a) {
   // (pieces 0-15 = A rows, 16-31 = B rows; 64 B per row; chunk c of row r at
   // slot c ^ ((r >> 2) & 3))
   auto issue = [&](int gs) {
-    if (gs >= ntiles * NSTG) return;
+    if (gs >= ntiles * NSTG || (PROBE_ABL & 1)) return;
     int qb, ct;
     tile_at(gs / NSTG, qb, ct);
     const int ks = gs % NSTG;
@@ -122,12 +125,14 @@ __global__ __launch_bounds__(256, 1) void probe(Args a) {
 #pragma unroll
         for (int rb = 0; rb < 4; rb++) {
           const int row = wr * 128 + rb * 32 + (ln & 31);
-          fa[rb] = *(const bf16x8 *)(st + row * 64 + ((chunk ^ ((row >> 2) & 3)) * 16));
+          if (PROBE_ABL & 2) { fa[rb] = (bf16x8){}; asm volatile("" : "+v"(fa[rb])); }
+          else fa[rb] = *(const bf16x8 *)(st + row * 64 + ((chunk ^ ((row >> 2) & 3)) * 16));
         }
 #pragma unroll
         for (int cb = 0; cb < 4; cb++) {
           const int row = wc * 128 + cb * 32 + (ln & 31);
-          fb[cb] = *(const bf16x8 *)(st + BM * 64 + row * 64 + ((chunk ^ ((row >> 2) & 3)) * 16));
+          if (PROBE_ABL & 2) { fb[cb] = (bf16x8){}; asm volatile("" : "+v"(fb[cb])); }
+          else fb[cb] = *(const bf16x8 *)(st + BM * 64 + row * 64 + ((chunk ^ ((row >> 2) & 3)) * 16));
         }
 #pragma unroll
         for (int rb = 0; rb < 4; rb++)
