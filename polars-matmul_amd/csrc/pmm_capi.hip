@@ -308,6 +308,17 @@ bool bf16_ws_enabled(int capg, int64_t d) {
   return capg <= kBf16WsMaxCapg && gemm_bf16_ws_lds_bytes(capg, dp) <= 160 * 1024;
 }
 
+// One-wave-per-SIMD 256-row bf16 kernel (pmm_bf16_r64_kernel.h): PMM_BF16_R64
+// (read per call; see DESIGN.md §3c for the default).  It needs capg <=
+// kBf16R64MaxCapg (k <= 192) and N < 2^26.
+bool bf16_r64_enabled(int64_t k, int64_t n, int64_t d) {
+  const char *e = getenv("PMM_BF16_R64");
+  if (!e || atoi(e) == 0) return false;
+  const int dp = (int)(cdiv(d, kBf16DAlign) * kBf16DAlign);
+  return next_pow2((int)k + 64, 128) <= kBf16R64MaxCapg && n < (1 << 26) && gemm_bf16_r64_lds_bytes(dp) > 0 &&
+         gemm_bf16_r64_lds_bytes(dp) <= 160 * 1024;
+}
+
 // 256-query-row bf16 kernel (pmm_bf16_dsx_kernel.h; padded D of 256, 512 or
 // 768, capg <= kBf16WsMaxCapg): lab build only, PMM_BF16_DSX=1 (read per
 // call).  Measured slower than the wave-specialised kernel at c4 (DESIGN.md
@@ -350,11 +361,13 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
     if (cap_env > 0 && k + 64 <= 512) p.capg = std::max<int>(((int)k + 64 + 7) / 8 * 8, std::min(cap_env, 512) / 8 * 8);
   }
   const bool bf16 = compute == PMM_COMPUTE_BF16;
-  const bool dsx = bf16 && bf16_dsx_enabled(p.capg, d);
-  const bool ws = bf16 && !dsx && bf16_ws_enabled(p.capg, d);
-  p.variant = bf16 ? (dsx ? -4 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
-  const int bm = bf16 ? (dsx ? kBf16DsxBM : kBf16BM) : gemm_f32_bm(p.variant);
-  const int bn = bf16 ? (dsx ? kBf16DsxBN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
+  const bool r64 = bf16 && bf16_r64_enabled(k, n, d);
+  if (r64) p.capg = next_pow2((int)k + 64, 128);  // (its compaction: 4 keys per lane)
+  const bool dsx = bf16 && !r64 && bf16_dsx_enabled(p.capg, d);
+  const bool ws = bf16 && !r64 && !dsx && bf16_ws_enabled(p.capg, d);
+  p.variant = bf16 ? (r64 ? -5 : dsx ? -4 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
+  const int bm = bf16 ? (r64 ? kBf16R64BM : dsx ? kBf16DsxBM : kBf16BM) : gemm_f32_bm(p.variant);
+  const int bn = bf16 ? (r64 ? kBf16R64BN : dsx ? kBf16DsxBN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
   const size_t cand_budget = size_t(8) << 30;
   int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
@@ -371,10 +384,10 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   // f32 kernel: the same split of units (PMM_F32_WHOLE=0: split units only).
   // At c3 the GEMM time is unchanged (1076 ms either way) and the merge reads
   // 0.89 GB instead of 2.17 GB (0.40 vs 0.65 ms).
-  const bool whole = bf16 ? ((ws || dsx) && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
+  const bool whole = bf16 ? ((ws || dsx || r64) && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
   // unit overhead in tiles: loading the unit's query rows into registers
   // (a dsx unit: 256 rows x D, about sixteen of its 16-column tiles' bytes)
-  plan_units(m, n, bm, bn, cus, bf16 ? (dsx ? 8.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
+  plan_units(m, n, bm, bn, cus, bf16 ? (dsx ? 8.0 : r64 ? 8.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
   // merge_kernel's per-row LDS capacity: at least 512, so a row's candidate
   // lists rarely need a compaction before the final one (c1: ~400 survivors
   // of the seed threshold per row; P = 128 compacted ~6 times, 23 us)
@@ -812,7 +825,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
       const int seed_env = getenv("PMM_BF16_SEED") ? atoi(getenv("PMM_BF16_SEED")) : 1;  // (read per call: tests toggle it)
       int64_t ns = kSeedMaxNs;
       if (const char *ne = getenv("PMM_SEED_NS")) ns = std::max<int64_t>(32, std::min<int64_t>(atoll(ne), kSeedMaxNs) / 32 * 32);
-      if (seed_env && (p.variant == -2 || p.variant == -4) && 4 * k <= ns && n >= 8 * ns &&
+      if (seed_env && (p.variant == -2 || p.variant == -4 || p.variant == -5) && 4 * k <= ns && n >= 8 * ns &&
           (size_t)m * ns * 4 <= p.off_qn - p.off_cand) {
         float *sample = (float *)(w + p.off_cand);
         Timed t("seed_bf16", s);
@@ -822,8 +835,13 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     }
     {
       // (the suffix names the kernel; pmm_timing_read matches substrings)
-      Timed t(p.variant == -4 ? "gemm_bf16_topk/dsx" : p.variant == -2 ? "gemm_bf16_topk/ws" : "gemm_bf16_topk/one-wave", s);
-      HIP_TRY(p.variant == -4   ? launch_gemm_bf16_dsx(a, p.grid, s)
+      Timed t(p.variant == -5   ? "gemm_bf16_topk/r64"
+              : p.variant == -4 ? "gemm_bf16_topk/dsx"
+              : p.variant == -2 ? "gemm_bf16_topk/ws"
+                                : "gemm_bf16_topk/one-wave",
+              s);
+      HIP_TRY(p.variant == -5   ? launch_gemm_bf16_r64(a, p.grid, s)
+              : p.variant == -4 ? launch_gemm_bf16_dsx(a, p.grid, s)
               : p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s)
                                 : launch_gemm_bf16(a, p.grid, s));
     }

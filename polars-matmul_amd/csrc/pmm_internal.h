@@ -152,6 +152,15 @@ bool bf16_dsx_supported(int D);  // D = padded dimension
 size_t gemm_bf16_dsx_lds_bytes(int D);
 hipError_t launch_gemm_bf16_dsx(const GemmF32Args &a, int grid, hipStream_t s);
 hipError_t launch_seed_bf16_dsx(const GemmF32Args &a, float *S, int ns, hipStream_t s);
+// 256-query-row bf16 kernel held by one wave per SIMD (pmm_bf16_r64_kernel.h):
+// 64 rows x D per wave (AGPRs + VGPRs), 32-column corpus tiles, the epilogue
+// on the same wave between the MFMAs.  The wave-specialised kernel's
+// arithmetic bit for bit (its seed serves both).  capg <= kBf16R64MaxCapg,
+// N < 2^26.
+constexpr int kBf16R64BM = 256, kBf16R64BN = 32;
+constexpr int kBf16R64MaxCapg = 256;  // its compaction holds 4 keys per lane (k <= 192)
+size_t gemm_bf16_r64_lds_bytes(int D);  // D = padded dimension; 0 if unsupported
+hipError_t launch_gemm_bf16_r64(const GemmF32Args &a, int grid, hipStream_t s);
 // f32 rows -> bf16 (round to nearest even) with row stride ldd, columns
 // d..ldd-1 zero-filled.
 hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t lds, uint16_t *dst,

@@ -965,3 +965,80 @@ def test_bf16_dsx_whole_blocks_and_splits(pmm, metric, monkeypatch):
     assert float((osc.double() - got_true).abs().max()) < 1e-4 * max(1.0, float(ref_s.abs().max()))
     srt = torch.sort(oi, dim=1).values
     assert bool((srt[:, 1:] != srt[:, :-1]).all())
+
+
+# ---- the one-wave-per-SIMD 256-row bf16 kernel (pmm_bf16_r64_kernel.h,
+# PMM_BF16_R64=1): the wave-specialised kernel's arithmetic, so both return the
+# same lists bit for bit (indices and f32 scores), and the truth check holds ----
+
+@pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (520, 40000, 768, 100), (70, 3000, 500, 192),
+                                     (257, 20011, 768, 100), (1, 1000, 256, 1), (600, 999, 700, 64),
+                                     (33, 70000, 128, 50), (130, 9000, 384, 120), (90, 5000, 640, 7)])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_r64_equals_ws(pmm, m, n, d, k, metric, monkeypatch):
+    rs = np.random.RandomState(m + n + d + k + 11)
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    c[n // 2:n // 2 + 20] = c[:20]  # exact ties across the corpus
+    q[m // 2] = 0.0                  # a zero-norm query row
+    monkeypatch.setenv("PMM_BF16_R64", "1")
+    ri, rsc = gpu_topk_bf16(q, c, k, metric)
+    _bf16_truth_check(q, c, k, metric, ri, rsc, f"bf16 r64 {m}x{n}x{d} k={k} {metric}")
+    monkeypatch.setenv("PMM_BF16_R64", "0")
+    wi, wsc = gpu_topk_bf16(q, c, k, metric)
+    assert np.array_equal(ri, wi)
+    assert np.array_equal(rsc.view(np.uint32), wsc.view(np.uint32))
+
+
+@pytest.mark.parametrize("metric", ["cosine", "euclidean", "dot"])
+def test_bf16_r64_whole_blocks_and_splits(pmm, metric, monkeypatch):
+    # PMM_CUS=16: 129 query blocks of 256 rows on 16 workgroups, so 128 run
+    # whole (row state carried across splits) and one as split units; the
+    # seed on (1M-scale thresholds are not needed for equality); bit-equal to
+    # the wave-specialised kernel on every row
+    import torch
+
+    monkeypatch.setenv("PMM_CUS", "16")
+    n = _native()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(29)
+    m, N, d, k = 33000, 12000, 512, 40
+    q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
+    c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
+    outs = []
+    for r64 in ("1", "0"):
+        monkeypatch.setenv("PMM_BF16_R64", r64)
+        oi = torch.empty((m, k), dtype=torch.int32, device=dev)
+        osc = torch.empty((m, k), dtype=torch.float32, device=dev)
+        n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS[metric],
+                           oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append((oi.cpu().numpy(), osc.cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+
+
+def test_bf16_r64_seeded_1m_rows_equal_ws(pmm, monkeypatch):
+    # a corpus long enough for the threshold seed (n >= 8 ns) and for
+    # compactions, queue overflows and catch-ups in early tiles: bit-equal
+    import torch
+
+    n = _native()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(31)
+    m, N, d, k = 2048, 300000, 768, 100
+    q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
+    c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
+    outs = []
+    for r64 in ("1", "0"):
+        monkeypatch.setenv("PMM_BF16_R64", r64)
+        oi = torch.empty((m, k), dtype=torch.int32, device=dev)
+        osc = torch.empty((m, k), dtype=torch.float32, device=dev)
+        n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS["cosine"],
+                           oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        outs.append((oi.cpu().numpy(), osc.cpu().numpy()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
