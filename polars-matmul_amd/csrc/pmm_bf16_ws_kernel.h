@@ -98,9 +98,19 @@ constexpr int QCAP = PMM_WS_QCAP;            // survivor queue per epilogue wave
 #define PMM_WS_EPI_OFFSET -1  // (A/B: -1 = by K steps (2 at KS >= 6, else 1); 0 = from the first interval)
 #endif
 #ifndef PMM_WS_DRAIN_TILES
-#define PMM_WS_DRAIN_TILES 4  // (a queued survivor's column norm must stay in the 8-tile ring: <= 6)
+#define PMM_WS_DRAIN_TILES 4  // (the survivor drain period; see drain_tiles below)
 #endif
-static_assert(PMM_WS_DRAIN_TILES >= 1 && PMM_WS_DRAIN_TILES <= 6, "survivor drain period");
+static_assert(PMM_WS_DRAIN_TILES >= 1, "survivor drain period");
+// A survivor of tile x is queued during tile x + 1 and re-scored with its
+// column norm from the CVT-tile ring, whose slot x is overwritten by the DMA
+// of tile x + CVT.  By the drain interval of tile D the DMA has reached tile
+// D + lead, lead = (drain interval + NST - 1) / KS: 2 or 3 tiles at KS >= 2,
+// but 4 at KS = 1 (one K-step per tile).  So the drain period P needs
+// P + lead < CVT: at KS = 1 the period 4 let the ring overwrite queued
+// survivors' norms (wrong cosine / euclidean scores at padded D = 128; found
+// by the bit-equality tests against the 256-row kernel) -- 2 there.
+template <int KS>
+constexpr int drain_tiles() { return KS == 1 ? (PMM_WS_DRAIN_TILES < 2 ? PMM_WS_DRAIN_TILES : 2) : PMM_WS_DRAIN_TILES; }
 #ifndef PMM_WS_NST
 #define PMM_WS_NST 7  // (A/B override: -DPMM_WS_NST=n)
 #endif
@@ -255,6 +265,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
   using namespace ws;
   using C = Carve<KS>;
   constexpr int NST = C::NST, NHB = C::NHB;
+  static_assert(drain_tiles<KS>() + (KS == 1 ? 4 : 3) < CVT, "queued survivors' column norms must stay in the ring");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   int *unit_l = (int *)(smem + OFF_UNIT);
   const int tid = threadIdx.x, lane = tid & 63;
@@ -620,7 +631,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             } else if (ks >= EO && (ks - EO) % ES == 0 && (ks - EO) / ES < NB) {
               epilogue(tile - 1, (ks - EO) / ES);
             }
-            if (ks == dks && ((tile - t0) % PMM_WS_DRAIN_TILES) == 0 && qlen > 0) {
+            if (ks == dks && ((tile - t0) % drain_tiles<KS>()) == 0 && qlen > 0) {
               wait_lgkm0();
               drain();
             }

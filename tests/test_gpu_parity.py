@@ -1042,3 +1042,18 @@ def test_bf16_r64_seeded_1m_rows_equal_ws(pmm, monkeypatch):
         outs.append((oi.cpu().numpy(), osc.cpu().numpy()))
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+
+
+@pytest.mark.parametrize("m", [33, 300])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_bf16_ws_d128_long_corpus_truth(pmm, m, metric, monkeypatch):
+    # padded D = 128 (one K-step per tile) over 2188 tiles: the wave-specialised
+    # kernel's survivor drain must run before the column-norm ring overwrites
+    # the queued survivors' norms (a 4-tile drain period did not: wrong cosine
+    # and euclidean scores in sparsely surviving row groups)
+    monkeypatch.setenv("PMM_BF16_R64", "0")
+    rs = np.random.RandomState(m + 5)
+    q = rs.randn(m, 128).astype(np.float32)
+    c = rs.randn(70000, 128).astype(np.float32)
+    idx, sc = gpu_topk_bf16(q, c, 50, metric)
+    _bf16_truth_check(q, c, 50, metric, idx, sc, f"bf16 ws d128 m={m} {metric}")

@@ -3,7 +3,7 @@
 # equality with the wave-specialised kernel), then c4 alternated r64 / ws.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -k "r64" --timeout 200 --timeout-method thread \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -k "r64 or d128" --timeout 200 --timeout-method thread \
   > gpurun_out/r64_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/r64_tests.log
 [ $rc -eq 0 ] || exit $rc
