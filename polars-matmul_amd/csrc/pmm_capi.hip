@@ -28,6 +28,9 @@ using namespace pmm;
 // (bf16_dsx_enabled is false outside it).
 hipError_t pmm::launch_gemm_bf16_dsx(const GemmF32Args &, int, hipStream_t) { return hipErrorNotSupported; }
 hipError_t pmm::launch_seed_bf16_dsx(const GemmF32Args &, float *, int, hipStream_t) { return hipErrorNotSupported; }
+// (the same for the one-wave 256-row kernel: bf16_r64_enabled is false)
+hipError_t pmm::launch_gemm_bf16_r64(const GemmF32Args &, int, hipStream_t) { return hipErrorNotSupported; }
+size_t pmm::gemm_bf16_r64_lds_bytes(int) { return 0; }
 #endif
 
 namespace {
@@ -308,10 +311,17 @@ bool bf16_ws_enabled(int capg, int64_t d) {
   return capg <= kBf16WsMaxCapg && gemm_bf16_ws_lds_bytes(capg, dp) <= 160 * 1024;
 }
 
-// One-wave-per-SIMD 256-row bf16 kernel (pmm_bf16_r64_kernel.h): PMM_BF16_R64
-// (read per call; see DESIGN.md §3c for the default).  It needs capg <=
-// kBf16R64MaxCapg (k <= 192) and N < 2^26.
+// One-wave-per-SIMD 256-row bf16 kernel (pmm_bf16_r64_kernel.h): lab build
+// only, PMM_BF16_R64=1 (read per call).  Measured slower than the
+// wave-specialised kernel at c4; kept as its bit-exact
+// cross-check.  It needs capg <= kBf16R64MaxCapg (k <= 192) and N < 2^26.
 bool bf16_r64_enabled(int64_t k, int64_t n, int64_t d) {
+#ifndef PMM_LAB
+  (void)k;
+  (void)n;
+  (void)d;
+  return false;
+#endif
   const char *e = getenv("PMM_BF16_R64");
   if (!e || atoi(e) == 0) return false;
   const int dp = (int)(cdiv(d, kBf16DAlign) * kBf16DAlign);

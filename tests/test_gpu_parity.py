@@ -967,10 +967,12 @@ def test_bf16_dsx_whole_blocks_and_splits(pmm, metric, monkeypatch):
     assert bool((srt[:, 1:] != srt[:, :-1]).all())
 
 
-# ---- the one-wave-per-SIMD 256-row bf16 kernel (pmm_bf16_r64_kernel.h,
-# PMM_BF16_R64=1): the wave-specialised kernel's arithmetic, so both return the
-# same lists bit for bit (indices and f32 scores), and the truth check holds ----
+# ---- the one-wave-per-SIMD 256-row bf16 kernel (pmm_bf16_r64_kernel.h; lab
+# build only, PMM_BF16_R64=1): the wave-specialised kernel's arithmetic, so
+# both return the same lists bit for bit (indices and f32 scores), and the
+# truth check holds ----
 
+@needs_lab
 @pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (520, 40000, 768, 100), (70, 3000, 500, 192),
                                      (257, 20011, 768, 100), (1, 1000, 256, 1), (600, 999, 700, 64),
                                      (33, 70000, 128, 50), (130, 9000, 384, 120), (90, 5000, 640, 7)])
@@ -990,6 +992,7 @@ def test_bf16_r64_equals_ws(pmm, m, n, d, k, metric, monkeypatch):
     assert np.array_equal(rsc.view(np.uint32), wsc.view(np.uint32))
 
 
+@needs_lab
 @pytest.mark.parametrize("metric", ["cosine", "euclidean", "dot"])
 def test_bf16_r64_whole_blocks_and_splits(pmm, metric, monkeypatch):
     # PMM_CUS=16: 129 query blocks of 256 rows on 16 workgroups, so 128 run
@@ -1019,6 +1022,7 @@ def test_bf16_r64_whole_blocks_and_splits(pmm, metric, monkeypatch):
     assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
 
 
+@needs_lab
 def test_bf16_r64_seeded_1m_rows_equal_ws(pmm, monkeypatch):
     # a corpus long enough for the threshold seed (n >= 8 ns) and for
     # compactions, queue overflows and catch-ups in early tiles: bit-equal

@@ -1,6 +1,8 @@
 #!/bin/bash
-# One-wave-per-SIMD 256-row bf16 kernel (PMM_BF16_R64): its GPU tests (bit
-# equality with the wave-specialised kernel), then c4 alternated r64 / ws.
+# One-wave-per-SIMD 256-row bf16 kernel (PMM_BF16_R64; lab build: run `make -C
+# polars-matmul_amd lab` first): its GPU tests (bit equality with the
+# wave-specialised kernel), then c4 alternated r64 / ws.
+export PMM_LIB=libpmm_lab.so
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -k "r64 or d128" --timeout 200 --timeout-method thread \
