@@ -81,6 +81,7 @@ struct MergeArgs {
   uint32_t *out_idx;
   float *out_score;
   int ablate;  // benchmarking only (PMM_MERGE_ABLATE): 1 = no selection/sort, 2 = no candidate loads
+  int no_rank;  // set by launch_merge: bitonic sort instead of rank counting (many rows)
 };
 
 struct RowSelArgs {

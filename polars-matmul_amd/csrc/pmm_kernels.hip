@@ -610,6 +610,28 @@ __device__ inline void wave_sort_desc_u64_pad(u64 *s, int P, int lane) {
   }
 }
 
+// Ranks of the n (<= 128) distinct keys a wave holds in slots lane (y0) and
+// 64 + lane (y1): r = the number of keys above it, by broadcasting each key
+// with v_readlane (no LDS round trips; see launch_merge for when it pays).
+__device__ inline u64 readlane_u64(u64 v, int j) {
+  return ((u64)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), j) << 32) |
+         (u64)(uint32_t)__builtin_amdgcn_readlane((uint32_t)v, j);
+}
+__device__ inline void wave_rank2(u64 y0, u64 y1, int n, int &r0, int &r1) {
+  r0 = 0;
+  r1 = 0;
+  const int n0 = n < 64 ? n : 64;
+  for (int j = 0; j < n0; j++) {
+    const u64 v = readlane_u64(y0, j);
+    r0 += v > y0;
+    r1 += v > y1;
+  }
+  for (int j = 64; j < n; j++) {
+    const u64 v = readlane_u64(y1, j - 64);
+    r0 += v > y0;
+    r1 += v > y1;
+  }
+}
 __device__ int merge_compact(u64 *scr, int cnt, int k, int P, u64 *T, int lane) {
   if (P <= 512 && cnt > k) {
     // select the k best (wave_kth_u64), keep them unordered
@@ -711,15 +733,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     }
   }
   wave_sync();
-  if (PMM_ABL(a.ablate) != 1) {
-    if (cnt > a.k_out && a.P <= 512) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
-    const int P2 = min(a.P, next_pow2_dev(cnt));
-    for (int i = cnt + lane; i < P2; i += 64) scr[MP(i)] = 0ull;
-    wave_sync();
-    wave_sort_desc_u64_pad(scr, P2, lane);
-  }
-  for (int j = lane; j < a.k_out; j += 64) {
-    const u64 x = (j < cnt) ? scr[MP(j)] : 0ull;
+  auto put = [&](int j, u64 x) __attribute__((always_inline)) {
     uint32_t id = 0xFFFFFFFFu;
     float sc = __uint_as_float(0x7FC00000u);
     if (x != 0ull) {
@@ -731,7 +745,27 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     }
     a.out_idx[(int64_t)row * a.k_out + j] = id;
     a.out_score[(int64_t)row * a.k_out + j] = sc;
+  };
+  if (PMM_ABL(a.ablate) != 1) {
+    if (cnt > a.k_out && a.P <= 512) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
+    if (a.k_out <= 128 && cnt <= a.k_out && !a.no_rank) {
+      // best-first by rank counting, no sort: each kept key goes to the
+      // position = the number of kept keys above it (keys are distinct)
+      const u64 y0 = lane < cnt ? scr[MP(lane)] : 0ull;
+      const u64 y1 = 64 + lane < cnt ? scr[MP(64 + lane)] : 0ull;
+      int r0, r1;
+      wave_rank2(y0, y1, cnt, r0, r1);
+      if (lane < cnt) put(r0, y0);
+      if (64 + lane < cnt) put(r1, y1);
+      for (int j = cnt + lane; j < a.k_out; j += 64) put(j, 0ull);
+      return;
+    }
+    const int P2 = min(a.P, next_pow2_dev(cnt));
+    for (int i = cnt + lane; i < P2; i += 64) scr[MP(i)] = 0ull;
+    wave_sync();
+    wave_sort_desc_u64_pad(scr, P2, lane);
   }
+  for (int j = lane; j < a.k_out; j += 64) put(j, (j < cnt) ? scr[MP(j)] : 0ull);
 }
 
 size_t merge_lds_bytes_per_wave(int P) { return (size_t)MPN(P) * 8; }
@@ -995,8 +1029,18 @@ hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const floa
   return launch_prologue_t<kMetricEuclidean>(a, grid, s);
 }
 
-hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s) {
-  if (a.M <= 0) return hipSuccess;
+constexpr int kMergeRankMaxRows = 16384;
+hipError_t launch_merge(const MergeArgs &a0, int loader, hipStream_t s) {
+  if (a0.M <= 0) return hipSuccess;
+  MergeArgs a = a0;
+  // Final order by rank counting when few rows run (their waves wait on the
+  // sort's dependent LDS round trips: c1, 1000 rows, 18 vs 21 us), by the
+  // bitonic sort otherwise (rank counting's ~8 vector instructions per kept
+  // key and lane cost more issue than the sort when every SIMD holds several
+  // rows: c3, 100k rows, 0.423 vs 0.403 ms; tools/experiments/merge_rank_ab.sh).
+  // PMM_MERGE_RANK: 0 never, 1 always, unset by row count.  Same output.
+  static const int rank_env = getenv("PMM_MERGE_RANK") ? atoi(getenv("PMM_MERGE_RANK")) : -1;
+  a.no_rank = rank_env == 0 || (rank_env < 0 && a.M > kMergeRankMaxRows);
   int wpb = (int)(65536 / merge_lds_bytes_per_wave(a.P));
   wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
   const size_t lds = (size_t)wpb * merge_lds_bytes_per_wave(a.P);

@@ -358,6 +358,46 @@ def test_device_api_sharded_merge_equals_full(pmm):
     assert np.array_equal(got_s, full_s)
 
 
+# ---- the list merge on random inputs against a NumPy merge: final order by
+# rank counting (k_out <= 128, up to 16384 rows) and by the bitonic sort
+# (k_out > 128, or more rows); ties in score, empty slots, fewer valid entries
+# than k_out, compactions during the load ----
+@pytest.mark.parametrize("m,lists,k_in,k_out,metric,empty,tied", [
+    (37, 3, 50, 20, 0, 0.0, False), (20, 1, 30, 20, 1, 0.0, False), (64, 8, 100, 100, 0, 0.0, True),
+    (16, 64, 16, 128, 1, 0.0, False), (16, 2, 700, 100, 2, 0.0, False), (16, 5, 400, 128, 0, 0.3, True),
+    (16, 4, 40, 100, 2, 0.5, False), (16, 9, 300, 1, 0, 0.0, True), (16, 64, 40, 64, 1, 0.2, True),
+    (8, 3, 300, 129, 0, 0.1, False), (8, 70, 10, 100, 0, 0.0, False), (300, 8, 128, 128, 2, 0.05, True),
+    (20000, 4, 64, 100, 0, 0.1, True)])
+def test_merge_random_lists(m, lists, k_in, k_out, metric, empty, tied):
+    import torch
+    n = _native()
+    rs = np.random.RandomState(m * 1000 + lists * 10 + k_out)
+    L = lists * k_in
+    idx = np.stack([rs.permutation(8 * L)[:L] * 512 + rs.randint(512) for _ in range(m)]).astype(np.uint32)
+    sc = (rs.randint(0, 40, size=idx.shape) / 40.0 if tied else rs.randn(*idx.shape)).astype(np.float32)
+    if metric == 2:
+        sc = np.abs(sc)
+    drop = rs.rand(*idx.shape) < empty
+    idx[drop] = 0xFFFFFFFF
+    sc[drop] = np.nan
+    dev = torch.device("cuda:0")
+    ti = torch.from_numpy(idx.reshape(m, lists, k_in).view(np.int32)).to(dev)
+    ts = torch.from_numpy(sc.reshape(m, lists, k_in)).to(dev)
+    oi = torch.full((m, k_out), 7, dtype=torch.int32, device=dev)
+    os_ = torch.full((m, k_out), 7.0, dtype=torch.float32, device=dev)
+    n.merge_device(ti.data_ptr(), ts.data_ptr(), m, lists, k_in, k_out, metric, oi.data_ptr(), os_.data_ptr())
+    torch.cuda.synchronize()
+    gi, gsc = oi.cpu().numpy().view(np.uint32), os_.cpu().numpy()
+    for r in range(m):
+        ok = idx[r] != 0xFFFFFFFF
+        fi, fs = idx[r][ok], sc[r][ok]
+        order = np.lexsort((fi, fs if metric == 2 else -fs))[:k_out]
+        nv = len(order)
+        assert np.array_equal(gi[r, :nv], fi[order]), f"row {r}"
+        assert np.array_equal(gsc[r, :nv], fs[order]), f"row {r}"
+        assert np.all(gi[r, nv:] == 0xFFFFFFFF) and np.all(np.isnan(gsc[r, nv:])), f"row {r}"
+
+
 def test_c5_shape_corpus_sharded_8way(pmm):
     # BASELINE configs[4] (1M x 10M x 1024 cosine k=100 on 8 GPUs, corpus
     # row-sharded) at a size one GPU checks in seconds: D = 1024, k = 100,
