@@ -592,6 +592,9 @@ hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid
 #define MP(i) (i)
 #define MPN(P) (P)
 #endif
+#ifndef PMM_MERGE_SEL_E
+#define PMM_MERGE_SEL_E 1
+#endif
 __device__ inline void wave_sort_desc_u64_pad(u64 *s, int P, int lane) {
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -632,18 +635,29 @@ __device__ inline void wave_rank2(u64 y0, u64 y1, int n, int &r0, int &r1) {
     r1 += v > y1;
   }
 }
+// the k best of the cnt (<= 64 E) keys in scr, unordered, to its front
+template <int E>
+__device__ inline int merge_select(u64 *scr, int cnt, int k, u64 *T, int lane) {
+  u64 x[E];
+#pragma unroll
+  for (int e = 0; e < E; e++) x[e] = (lane + 64 * e < cnt) ? scr[MP(lane + 64 * e)] : 0ull;
+  wave_sync();  // every lane has read before any rewrites
+  const u64 t = wave_kth_u64<E>(x, k);
+  if (t > *T) *T = t;
+  cnt = wave_keep_ge<E>(x, t, [&](int pos, u64 v) __attribute__((always_inline)) { scr[MP(pos)] = v; }, lane);
+  wave_sync();
+  return cnt;
+}
+
 __device__ int merge_compact(u64 *scr, int cnt, int k, int P, u64 *T, int lane) {
   if (P <= 512 && cnt > k) {
-    // select the k best (wave_kth_u64), keep them unordered
-    u64 x[8];
-#pragma unroll
-    for (int e = 0; e < 8; e++) x[e] = (lane + 64 * e < cnt) ? scr[MP(lane + 64 * e)] : 0ull;
-    wave_sync();  // every lane has read before any rewrites
-    const u64 t = wave_kth_u64<8>(x, k);
-    if (t > *T) *T = t;
-    cnt = wave_keep_ge<8>(x, t, [&](int pos, u64 v) __attribute__((always_inline)) { scr[MP(pos)] = v; }, lane);
-    wave_sync();
-    return cnt;
+    // select the k best (wave_kth_u64) over as few key slots per lane as
+    // hold cnt: its cost is a compare per slot per bit
+#if PMM_MERGE_SEL_E
+    if (cnt <= 128) return merge_select<2>(scr, cnt, k, T, lane);
+    if (cnt <= 256) return merge_select<4>(scr, cnt, k, T, lane);
+#endif
+    return merge_select<8>(scr, cnt, k, T, lane);
   }
   for (int i = cnt + lane; i < P; i += 64) scr[MP(i)] = 0ull;
   wave_sync();
