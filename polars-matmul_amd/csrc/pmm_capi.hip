@@ -397,6 +397,9 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   const bool whole = bf16 ? ((ws || dsx || r64) && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
   // unit overhead in tiles: loading the unit's query rows into registers
   // (a dsx unit: 256 rows x D, about sixteen of its 16-column tiles' bytes)
+  // (Two 128 x 128 f32 workgroups per CU -- 196 registers and 74 KiB of LDS
+  // let them co-reside -- planned for 512 slots measured slower at c1: 0.129
+  // vs 0.118 ms, profiles/r3_c1/wpc_variant_ab.txt.)
   plan_units(m, n, bm, bn, cus, bf16 ? (dsx ? 8.0 : r64 ? 8.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
   // merge_kernel's per-row LDS capacity: at least 512, so a row's candidate
   // lists rarely need a compaction before the final one (c1: ~400 survivors

@@ -676,8 +676,12 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wpb = blockDim.x >> 6;
-  const int row = blockIdx.x * wpb + wid;
-  if (row >= a.M) return;  // whole wave exits; no block-wide barriers below
+  const int rpos = blockIdx.x * wpb + wid;
+  if (rpos >= a.M) return;  // whole wave exits; no block-wide barriers below
+  // kMergeReverse: the split units' rows (many segments each) sit after the
+  // whole query blocks' rows (one segment); started first, the long rows no
+  // longer form the launch's tail
+  const int row = (a.flags & kMergeReverse) ? a.M - 1 - rpos : rpos;
   u64 *scr = (u64 *)smem + (size_t)wid * MPN(a.P);
   u64 T = (LOADER == 0) ? a.gthr[row] : 0ull;
   int cnt = 0;
@@ -718,8 +722,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
       s++;
       ns = (s < a.S) ? __builtin_amdgcn_readlane(nl, s) : 0;
     }
-    while (s < a.S) {
-      u64 x[MU];
+    auto fetch = [&](u64(&x)[MU]) __attribute__((always_inline)) {
 #pragma unroll
       for (int u = 0; u < MU; u++) {
         x[u] = 0ull;
@@ -734,8 +737,30 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
           }
         }
       }
+    };
+    if (a.flags & kMergePipelined) {
+      // the next batch's loads go out before this one is taken (a row's
+      // batches no longer pay one memory latency each)
+      if (s < a.S) {
+        u64 x[MU], y[MU];
+        fetch(x);
+        for (;;) {
+          const bool more = s < a.S;
+          if (more) fetch(y);
 #pragma unroll
-      for (int u = 0; u < MU; u++) take(x[u]);
+          for (int u = 0; u < MU; u++) take(x[u]);
+          if (!more) break;
+#pragma unroll
+          for (int u = 0; u < MU; u++) x[u] = y[u];
+        }
+      }
+    } else {
+      while (s < a.S) {
+        u64 x[MU];
+        fetch(x);
+#pragma unroll
+        for (int u = 0; u < MU; u++) take(x[u]);
+      }
     }
   } else {
     for (int s = 0; s < a.S; s++) {
@@ -1055,6 +1080,11 @@ hipError_t launch_merge(const MergeArgs &a0, int loader, hipStream_t s) {
   // PMM_MERGE_RANK: 0 never, 1 always, unset by row count.  Same output.
   static const int rank_env = getenv("PMM_MERGE_RANK") ? atoi(getenv("PMM_MERGE_RANK")) : -1;
   a.no_rank = rank_env == 0 || (rank_env < 0 && a.M > kMergeRankMaxRows);
+  // Rows last to first and the next candidate batch in flight while one is
+  // taken: c3 0.439 ms against 0.523 (reverse alone 0.506, pipelined alone
+  // 0.450; alternated on one box, profiles/r3_merge/flags_ab.txt).  Same
+  // output.  PMM_MERGE_FLAGS (read per call) overrides, for A/Bs.
+  a.flags = getenv("PMM_MERGE_FLAGS") ? atoi(getenv("PMM_MERGE_FLAGS")) : (kMergeReverse | kMergePipelined);
   int wpb = (int)(65536 / merge_lds_bytes_per_wave(a.P));
   wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
   const size_t lds = (size_t)wpb * merge_lds_bytes_per_wave(a.P);

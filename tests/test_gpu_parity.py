@@ -470,6 +470,28 @@ def test_whole_query_block_schedule(pmm, compute, monkeypatch):
     assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
 
 
+@pytest.mark.parametrize("flags", ["0", "1", "2", "3"])
+def test_merge_schedules_same_lists(pmm, flags, monkeypatch):
+    # merge_kernel's row order (kMergeReverse) and pipelined candidate loads
+    # (kMergePipelined) change when work happens, never the result: whole-block
+    # rows (one segment) and split rows (many segments, several batches each)
+    # under every combination equal the default, which equals the oracle
+    import oracle
+
+    rs = np.random.RandomState(31)
+    m, N, d, k = 1200, 20000, 64, 100
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(N, d).astype(np.float32)
+    monkeypatch.setenv("PMM_CUS", "4")  # 10 query blocks: 8 whole, 2 as split units
+    want = gpu_topk(q, c, k, "cosine")
+    monkeypatch.setenv("PMM_MERGE_FLAGS", flags)
+    got = gpu_topk(q, c, k, "cosine")
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    rows = np.arange(0, m, 97)
+    oi, osc = oracle.topk(q[rows], c, k, oracle.COSINE)
+    assert_bitexact(got[0][rows], got[1][rows], oi, osc, label=f"merge flags {flags}")
+
+
 def test_merge_bytes_counts_the_candidates_left(pmm):
     # the reduction's algorithmic bytes (bench.py "reduction_roofline"):
     # counts + thresholds + output, plus 8 B per candidate the GEMM left --
