@@ -299,6 +299,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     // of the first two MFMA groups: c1 0.141 vs 0.143 ms, c2 0.134 vs 0.136;
     // 2 behind each of four groups 0.146 / 0.139)
     constexpr int NPART = (NB == 4 && NW == 4) ? PMM_F32_DMA_PARTS_SMALL : PMM_F32_DMA_PARTS;
+#ifndef PMM_F32_FRAG_PREFETCH
+#define PMM_F32_FRAG_PREFETCH 1  // (A/B: 0 off, 1 the 128 x 128 variant only, 2 every variant)
+#endif
+    constexpr bool FPF = PMM_F32_FRAG_PREFETCH == 2 || (PMM_F32_FRAG_PREFETCH == 1 && NB == 4 && NW == 4);
+    // (one ballot per 32 x 32 block before the per-score ones -- the max of
+    // the pre-filter differences -- measured flat at c3 in round 2 and slower
+    // at c1 in round 3: 0.083-0.085 vs 0.082 ms,
+    // profiles/r3_c1/block_prefilter_ab.txt)
     static_assert(TP % NPART == 0 && NPART <= 4, "DMA pieces split evenly over the MFMA groups");
     __amdgpu_buffer_rsrc_t rb = rsrc_b(t0);
     stage(buf, rb, 0, t0, 0, TP);
@@ -320,21 +328,34 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       auto kstep = [&](int ks, auto DEF, auto PREV) __attribute__((always_inline)) {
         __syncthreads();  // stage `buf` landed (vmcnt(0) + barrier); buf^1 free
         const char *st = smem + buf * G::STAGE;
-#pragma unroll
-        for (int qd = 0; qd < 4; qd++) {
-          // KORDER 0: lane half h covers k = 16h..16h+15 (substep j of group
-          // qd pairs k = 4qd+j with 16+4qd+j).  Otherwise half h reads chunk
-          // 2qd+h: from a gathered image element j is k = 8qd+h+2j, so
-          // substep t = 4qd+j pairs k = 2t (h = 0) with 2t+1 (h = 1) -- every
-          // output is the k-ordered fmaf chain of the oracle bit for bit; from
-          // a plain image (k = 8qd+4h..+3) two v_permlane32_swap trade the
-          // lower half's odd k for the upper half's even k, leaving registers
-          // {0,2,1,3} = k pairs (8qd,+1) (8qd+2,+3) (8qd+4,+5) (8qd+6,+7).
+        // KORDER 0: lane half h covers k = 16h..16h+15 (substep j of group
+        // qd pairs k = 4qd+j with 16+4qd+j).  Otherwise half h reads chunk
+        // 2qd+h: from a gathered image element j is k = 8qd+h+2j, so
+        // substep t = 4qd+j pairs k = 2t (h = 0) with 2t+1 (h = 1) -- every
+        // output is the k-ordered fmaf chain of the oracle bit for bit; from
+        // a plain image (k = 8qd+4h..+3) two v_permlane32_swap trade the
+        // lower half's odd k for the upper half's even k, leaving registers
+        // {0,2,1,3} = k pairs (8qd,+1) (8qd+2,+3) (8qd+4,+5) (8qd+6,+7).
+        auto rd_frag = [&](int qd, f32x4 &av, f32x4 (&b)[NB]) __attribute__((always_inline)) {
           const int co = KO == 0 ? 16 * ((4 * h + qd) ^ swz) : 16 * ((2 * qd + h) ^ swz);
-          f32x4 av = *(const f32x4 *)(st + a_rd + co);
-          f32x4 b[NB];
+          av = *(const f32x4 *)(st + a_rd + co);
 #pragma unroll
           for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
+        };
+        // FPF: group qd + 1's fragments are read before group qd's MFMAs, so
+        // only a K step's first group waits on a fresh LDS read (one wave per
+        // SIMD has no partner wave to cover that latency)
+        f32x4 avs[FPF ? 2 : 1], bs[FPF ? 2 : 1][NB];
+        if (FPF) rd_frag(0, avs[0], bs[0]);
+#pragma unroll
+        for (int qd = 0; qd < 4; qd++) {
+          if (FPF && qd < 3) {
+            rd_frag(qd + 1, avs[(qd + 1) & 1], bs[(qd + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);  // (hipcc would sink the reads to the group's end)
+          }
+          if (!FPF) rd_frag(qd, avs[0], bs[0]);
+          f32x4 &av = avs[FPF ? (qd & 1) : 0];
+          f32x4(&b)[NB] = bs[FPF ? (qd & 1) : 0];
           constexpr bool A_SWAP = KO == 1 || KO == 3;
           constexpr bool B_SWAP = KO == 1;
           auto kpair = [](f32x4 &x) __attribute__((always_inline)) {
@@ -452,13 +473,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           const int gcol = col0 + 32 * c + r32;
           const bool cvalid = gcol < a.N;
           const float cv = XFORM ? cvt[32 * c + r32] : 0.0f;
+          auto prefilter = [&](int e) __attribute__((always_inline)) {
+            const float v = acc[c][e];
+            if (METRIC == kMetricDot) return v;
+            if (METRIC == kMetricCosine) return v * cv;
+            return fmaf(2.0f, v, -cv);
+          };
 #pragma unroll
           for (int e = 0; e < 16; e++) {
             const float v = acc[c][e];
-            float pv;
-            if (METRIC == kMetricDot) pv = v;
-            else if (METRIC == kMetricCosine) pv = v * cv;
-            else pv = fmaf(2.0f, v, -cv);
+            const float pv = prefilter(e);
             const bool p = cvalid && !(pv < lo[e]);
             const u64 m = __ballot(p);
             if (m == 0ull) continue;

@@ -7,8 +7,8 @@ out=gpurun_out/lib_ab.txt
 : > $out
 for rep in 1 2; do
   for lib in "$@"; do
-    for cfg in c3 c1 c4; do
-      if [ $cfg = c1 ]; then st="--steps 400 --warmup 20"; else st="--steps 3 --warmup 1"; fi
+    for cfg in ${CFGS:-c3 c1 c4}; do
+      if [ $cfg = c1 ] || [ $cfg = c2 ]; then st="--steps 400 --warmup 20"; else st="--steps 3 --warmup 1"; fi
       PMM_LIB=$lib timeout -k 10 180 python -u bench.py --config $cfg $st --extra none --cpu-sample 0 \
         --boundary 0 --check 8 > gpurun_out/libab.json 2> gpurun_out/libab_err.log || exit 1
       python - $lib $cfg gpurun_out/libab.json >> $out <<'PY'
