@@ -290,9 +290,25 @@ int choose_variant(int mode, int capg, int64_t m = 1 << 30, int64_t n = 1 << 30,
     const char *e = getenv("PMM_GEMM_VARIANT");
     env = e ? atoi(e) : -1;
   }
-  if (env >= 0 && env < 4 && gemm_f32_lds_bytes(env, mode, capg) <= 160 * 1024) return env;
-  if (cdiv(m, 256) * cdiv(n, 256) < 4 * (int64_t)cus && gemm_f32_lds_bytes(0, mode, capg) <= 160 * 1024)
+  if (env >= 0 && env < 5 && gemm_f32_lds_bytes(env, mode, capg) <= 160 * 1024) return env;
+  if (cdiv(m, 256) * cdiv(n, 256) < 4 * (int64_t)cus && gemm_f32_lds_bytes(0, mode, capg) <= 160 * 1024) {
+    // 128 x 128 tiles, or for the fused top-k 128 x 64 (variant 4) when its
+    // finer units give a shorter makespan: per unit, tps tiles of bn / 128
+    // (128-column tile times, the thin tile's extra overhead at 12%) plus
+    // half a tile of unit start.  c1: 3 tiles per unit on 216 CUs, or 5 thin
+    // tiles on 256 -> fused kernel 82 -> 76 us, c2 80 -> 74-75
+    // (profiles/r3_c1/variant4_ab.txt).
+    if (mode == 0 && gemm_f32_lds_bytes(4, mode, capg) <= 160 * 1024) {
+      auto makespan = [&](int v) {
+        Plan q;
+        plan_units(m, n, gemm_f32_bm(v), gemm_f32_bn(v), cus, 0.5, 1 << 20, q);
+        const double tile = gemm_f32_bn(v) / 128.0 * (v == 4 ? 1.12 : 1.0);
+        return (double)cdiv(q.units, cus) * (q.tps * tile + 0.5);
+      };
+      if (makespan(4) < makespan(0)) return 4;
+    }
     return 0;
+  }
   // measured on c3 (100k x 1M x 768 cosine k=100): v3 136.9, v2 133.1, v1 120.5 TFLOP/s
   static const int order[4] = {3, 2, 0, 1};
   for (int v : order)

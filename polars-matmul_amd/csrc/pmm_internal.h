@@ -82,10 +82,11 @@ struct MergeArgs {
   float *out_score;
   int ablate;  // benchmarking only (PMM_MERGE_ABLATE): 1 = no selection/sort, 2 = no candidate loads
   int no_rank;  // set by launch_merge: bitonic sort instead of rank counting (many rows)
-  int flags;    // set by launch_merge: kMergeReverse, kMergePipelined
+  int flags;    // set by launch_merge: kMergeReverse, kMergePipelined, kMergeSplitRow
 };
 constexpr int kMergeReverse = 1;    // rows last to first (split rows, the heavy ones, start first)
 constexpr int kMergePipelined = 2;  // next candidate batch's loads in flight while one is taken
+constexpr int kMergeSplitRow = 4;   // a block of 4 waves per row, each merging a quarter of its lists
 
 struct RowSelArgs {
   const void *scores;   // [rows][lds] f32 or f64, already metric-transformed

@@ -104,9 +104,10 @@ struct GemmShape {
 // Tile-shape variants compiled in (index = GemmVariant id).
 //   0: NB=4 NW=4 (128 x 128, 1 wave/SIMD)   1: NB=8 NW=4 (128 x 256)
 //   2: NB=4 NW=8 (256 x 128, 2 waves/SIMD)  3: NB=8 NW=8 (256 x 256)
-constexpr int kGemmVariants = 4;
-constexpr int kVarNB[kGemmVariants] = {4, 8, 4, 8};
-constexpr int kVarNW[kGemmVariants] = {4, 4, 8, 8};
+//   4: NB=2 NW=4 (128 x 64, 1 wave/SIMD: finer units for small problems)
+constexpr int kGemmVariants = 5;
+constexpr int kVarNB[kGemmVariants] = {4, 8, 4, 8, 2};
+constexpr int kVarNW[kGemmVariants] = {4, 4, 8, 8, 4};
 
 int gemm_f32_bm(int variant) { return 32 * kVarNW[variant]; }
 int gemm_f32_bn(int variant) { return 32 * kVarNB[variant]; }
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   // a row (physical chunk p>>2, element j = p&3) holds logical chunk
   // ch = (p>>2) ^ swizzle, i.e. k = 8*(ch>>1) + (ch&1) + 2j.  Plain image
   // (16-byte pieces of 1 KiB = 8 rows): chunk ch of a row at ch ^ swizzle.
-  constexpr int KO = (NB == 4 && NW == 4) ? PMM_F32_KORDER_SMALL : PMM_F32_KORDER;
+  constexpr int KO = (NB <= 4 && NW == 4) ? PMM_F32_KORDER_SMALL : PMM_F32_KORDER;
   constexpr bool A_GATHER = KO == 2;
   constexpr bool B_GATHER = KO == 2 || KO == 3;
   constexpr int AP = A_GATHER ? 16 : 4, APIECE = A_GATHER ? 256 : 1024, ADW = A_GATHER ? 4 : 16;
@@ -298,11 +299,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     // cover this wave's DMA issue; its 8 pieces per step go out 4 behind each
     // of the first two MFMA groups: c1 0.141 vs 0.143 ms, c2 0.134 vs 0.136;
     // 2 behind each of four groups 0.146 / 0.139)
-    constexpr int NPART = (NB == 4 && NW == 4) ? PMM_F32_DMA_PARTS_SMALL : PMM_F32_DMA_PARTS;
+    constexpr int NPART = (NB <= 4 && NW == 4) ? PMM_F32_DMA_PARTS_SMALL : PMM_F32_DMA_PARTS;
 #ifndef PMM_F32_FRAG_PREFETCH
 #define PMM_F32_FRAG_PREFETCH 1  // (A/B: 0 off, 1 the 128 x 128 variant only, 2 every variant)
 #endif
-    constexpr bool FPF = PMM_F32_FRAG_PREFETCH == 2 || (PMM_F32_FRAG_PREFETCH == 1 && NB == 4 && NW == 4);
+    constexpr bool FPF = PMM_F32_FRAG_PREFETCH == 2 || (PMM_F32_FRAG_PREFETCH == 1 && NB <= 4 && NW == 4);
     // (one ballot per 32 x 32 block before the per-score ones -- the max of
     // the pre-filter differences -- measured flat at c3 in round 2 and slower
     // at c1 in round 3: 0.083-0.085 vs 0.082 ms,
@@ -576,6 +577,7 @@ hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid
     case 1: return launch_gemm_f32_v<8, 4>(a, mode, grid, lds, s);
     case 2: return launch_gemm_f32_v<4, 8>(a, mode, grid, lds, s);
     case 3: return launch_gemm_f32_v<8, 8>(a, mode, grid, lds, s);
+    case 4: return launch_gemm_f32_v<2, 4>(a, mode, grid, lds, s);
     default: return hipErrorInvalidValue;
   }
 }
@@ -695,17 +697,26 @@ __device__ int merge_compact(u64 *scr, int cnt, int k, int P, u64 *T, int lane) 
   return cnt;
 }
 
-template <int LOADER>
+template <int LOADER, bool SPLIT>
 __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wpb = blockDim.x >> 6;
-  const int rpos = blockIdx.x * wpb + wid;
-  if (rpos >= a.M) return;  // whole wave exits; no block-wide barriers below
+  // kMergeSplitRow (few rows, many lists, k <= 64): the block's 4 waves take
+  // one row, wave w merging lists [S w / 4, S (w + 1) / 4) down to its k best;
+  // wave 0 then selects the row's k best of those 4 lists.  Otherwise one
+  // wave per row; the only block-wide barrier is the split mode's, where
+  // every wave of the block has a row (grid = M).
+  // (a template parameter: the one-wave-per-row instantiation keeps its
+  // registers -- a runtime flag cost it an occupancy step, c3 0.57 vs 0.44 ms)
+  constexpr bool split = SPLIT;
+  const int rpos = split ? (int)blockIdx.x : (int)blockIdx.x * wpb + wid;
+  if (rpos >= a.M) return;  // whole wave exits
   // kMergeReverse: the split units' rows (many segments each) sit after the
   // whole query blocks' rows (one segment); started first, the long rows no
   // longer form the launch's tail
   const int row = (a.flags & kMergeReverse) ? a.M - 1 - rpos : rpos;
+  const int s_lo = split ? a.S * wid / 4 : 0, s_hi = split ? a.S * (wid + 1) / 4 : a.S;
   u64 *scr = (u64 *)smem + (size_t)wid * MPN(a.P);
   u64 T = (LOADER == 0) ? a.gthr[row] : 0ull;
   int cnt = 0;
@@ -739,25 +750,28 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     // sums + a binary search per slot -- measured the same at c1 and 29%
     // slower at c3.)
     constexpr int MU = 4;  // (8 and 16 in flight measured the same at c1 and c3)
-    const int nl = (lane < a.S) ? ((LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + lane] : a.k_in) : 0;
-    int s = 0, c = 0;
-    int ns = __builtin_amdgcn_readlane(nl, 0);
-    while (s < a.S && c >= ns) {  // first non-empty list
+    // (lists [s_lo, s_hi): lane j holds list s_lo + j's length)
+    const int nl = (s_lo + lane < s_hi)
+                       ? ((LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + s_lo + lane] : a.k_in)
+                       : 0;
+    int s = s_lo, c = 0;
+    int ns = __builtin_amdgcn_readlane(nl, 0);  // (0 when the wave has no list)
+    while (s < s_hi && c >= ns) {  // first non-empty list
       s++;
-      ns = (s < a.S) ? __builtin_amdgcn_readlane(nl, s) : 0;
+      ns = (s < s_hi) ? __builtin_amdgcn_readlane(nl, s - s_lo) : 0;
     }
     auto fetch = [&](u64(&x)[MU]) __attribute__((always_inline)) {
 #pragma unroll
       for (int u = 0; u < MU; u++) {
         x[u] = 0ull;
-        if (s < a.S) {
+        if (s < s_hi) {
           const int i = c + lane;
           if (i < ns) x[u] = load_x(s, i);
           c += 64;
-          while (s < a.S && c >= ns) {
+          while (s < s_hi && c >= ns) {
             s++;
             c = 0;
-            ns = (s < a.S) ? __builtin_amdgcn_readlane(nl, s) : 0;
+            ns = (s < s_hi) ? __builtin_amdgcn_readlane(nl, s - s_lo) : 0;
           }
         }
       }
@@ -765,11 +779,11 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     if (a.flags & kMergePipelined) {
       // the next batch's loads go out before this one is taken (a row's
       // batches no longer pay one memory latency each)
-      if (s < a.S) {
+      if (s < s_hi) {
         u64 x[MU], y[MU];
         fetch(x);
         for (;;) {
-          const bool more = s < a.S;
+          const bool more = s < s_hi;
           if (more) fetch(y);
 #pragma unroll
           for (int u = 0; u < MU; u++) take(x[u]);
@@ -779,7 +793,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
         }
       }
     } else {
-      while (s < a.S) {
+      while (s < s_hi) {
         u64 x[MU];
         fetch(x);
 #pragma unroll
@@ -787,7 +801,7 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
       }
     }
   } else {
-    for (int s = 0; s < a.S; s++) {
+    for (int s = s_lo; s < s_hi; s++) {
       const int n_s = (LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + s] : a.k_in;
       for (int i0 = 0; i0 < n_s; i0 += 64) {
         const int i = i0 + lane;
@@ -809,6 +823,27 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     a.out_idx[(int64_t)row * a.k_out + j] = id;
     a.out_score[(int64_t)row * a.k_out + j] = sc;
   };
+  if (split) {
+    // each wave's k best (k <= 64: one slot per lane), then wave 0 takes the
+    // row's k best of the four lists into its own scratch
+    if (cnt > a.k_out) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
+    int *cnts = (int *)((u64 *)smem + (size_t)4 * MPN(a.P));
+    if (lane == 0) cnts[wid] = cnt;
+    __syncthreads();
+    if (wid != 0) return;
+    u64 x[4];
+    int tot = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const int ce = cnts[e];
+      x[e] = lane < ce ? ((const u64 *)smem + (size_t)e * MPN(a.P))[MP(lane)] : 0ull;
+      tot += ce;
+    }
+    wave_sync();  // every lane has read before wave 0's scratch is rewritten
+    const u64 t = tot > a.k_out ? wave_kth_u64<4>(x, a.k_out) : 1ull;
+    cnt = wave_keep_ge<4>(x, t, [&](int pos, u64 v) __attribute__((always_inline)) { scr[MP(pos)] = v; }, lane);
+    wave_sync();
+  }
   if (PMM_ABL(a.ablate) != 1) {
     if (cnt > a.k_out && a.P <= 512) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
     if (a.k_out <= 128 && cnt <= a.k_out && !a.no_rank) {
@@ -1108,22 +1143,33 @@ hipError_t launch_merge(const MergeArgs &a0, int loader, hipStream_t s) {
   // taken: c3 0.439 ms against 0.523 (reverse alone 0.506, pipelined alone
   // 0.450; alternated on one box, profiles/r3_merge/flags_ab.txt).  Same
   // output.  PMM_MERGE_FLAGS (read per call) overrides, for A/Bs.
-  a.flags = getenv("PMM_MERGE_FLAGS") ? atoi(getenv("PMM_MERGE_FLAGS")) : (kMergeReverse | kMergePipelined);
+  a.flags = getenv("PMM_MERGE_FLAGS") ? atoi(getenv("PMM_MERGE_FLAGS"))
+                                     : (kMergeReverse | kMergePipelined | kMergeSplitRow);
+  // four waves per row where rows are few and each has many lists to merge
+  // (c1: 1000 rows x 27 lists, one wave per SIMD otherwise) and the per-wave
+  // lists fit one slot per lane (k <= 64)
+  if (!(a.S >= 8 && a.k_out <= 64 && a.P <= 512 && !a.no_rank && a.ablate == 0)) a.flags &= ~kMergeSplitRow;
+  const bool split = (a.flags & kMergeSplitRow) != 0;
   int wpb = (int)(65536 / merge_lds_bytes_per_wave(a.P));
-  wpb = wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb);
-  const size_t lds = (size_t)wpb * merge_lds_bytes_per_wave(a.P);
-  const unsigned grid = (unsigned)((a.M + wpb - 1) / wpb);
-  if (lds > 65536) {  // (P = 8192 with the padding: 66 KiB)
+  wpb = split ? 4 : (wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb));
+  const size_t lds = (size_t)wpb * merge_lds_bytes_per_wave(a.P) + (split ? 16 : 0);
+  const unsigned grid = split ? (unsigned)a.M : (unsigned)((a.M + wpb - 1) / wpb);
+  if (lds > 65536) {  // (P = 8192 with the padding: 66 KiB; never in split mode)
     static bool attr_set[2] = {false, false};
     if (!attr_set[loader]) {
-      const void *fn = loader == 0 ? (const void *)merge_kernel<0> : (const void *)merge_kernel<1>;
+      const void *fn = loader == 0 ? (const void *)merge_kernel<0, false> : (const void *)merge_kernel<1, false>;
       hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       if (e != hipSuccess) return e;
       attr_set[loader] = true;
     }
   }
-  if (loader == 0) merge_kernel<0><<<grid, wpb * 64, lds, s>>>(a);
-  else merge_kernel<1><<<grid, wpb * 64, lds, s>>>(a);
+  if (split) {
+    if (loader == 0) merge_kernel<0, true><<<grid, wpb * 64, lds, s>>>(a);
+    else merge_kernel<1, true><<<grid, wpb * 64, lds, s>>>(a);
+  } else {
+    if (loader == 0) merge_kernel<0, false><<<grid, wpb * 64, lds, s>>>(a);
+    else merge_kernel<1, false><<<grid, wpb * 64, lds, s>>>(a);
+  }
   return hipGetLastError();
 }
 

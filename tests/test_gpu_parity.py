@@ -470,19 +470,26 @@ def test_whole_query_block_schedule(pmm, compute, monkeypatch):
     assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
 
 
-@pytest.mark.parametrize("flags", ["0", "1", "2", "3"])
-def test_merge_schedules_same_lists(pmm, flags, monkeypatch):
-    # merge_kernel's row order (kMergeReverse) and pipelined candidate loads
-    # (kMergePipelined) change when work happens, never the result: whole-block
-    # rows (one segment) and split rows (many segments, several batches each)
-    # under every combination equal the default, which equals the oracle
+@pytest.mark.parametrize("flags", ["0", "1", "2", "3", "4", "7"])
+@pytest.mark.parametrize("shape", ["whole+split", "many-lists"])
+def test_merge_schedules_same_lists(pmm, flags, shape, monkeypatch):
+    # merge_kernel's row order (kMergeReverse), pipelined candidate loads
+    # (kMergePipelined) and four waves per row (kMergeSplitRow, few rows with
+    # many lists and k <= 64) change when and where work happens, never the
+    # result: every combination equals the default, which equals the oracle.
+    # "whole+split": whole-block rows (one segment) and split rows (many
+    # segments, several batches each); "many-lists": the c1 shape's schedule
+    # (every row split over dozens of corpus ranges, k = 10)
     import oracle
 
     rs = np.random.RandomState(31)
-    m, N, d, k = 1200, 20000, 64, 100
+    if shape == "whole+split":
+        m, N, d, k = 1200, 20000, 64, 100
+        monkeypatch.setenv("PMM_CUS", "4")  # 10 query blocks: 8 whole, 2 as split units
+    else:
+        m, N, d, k = 700, 30011, 96, 10
     q = rs.randn(m, d).astype(np.float32)
     c = rs.randn(N, d).astype(np.float32)
-    monkeypatch.setenv("PMM_CUS", "4")  # 10 query blocks: 8 whole, 2 as split units
     want = gpu_topk(q, c, k, "cosine")
     monkeypatch.setenv("PMM_MERGE_FLAGS", flags)
     got = gpu_topk(q, c, k, "cosine")
