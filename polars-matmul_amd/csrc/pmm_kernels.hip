@@ -133,13 +133,15 @@ size_t gemm_f32_lds_bytes(int variant, int mode, int capg) {
 #ifndef PMM_F32_KORDER
 #define PMM_F32_KORDER 2
 #endif
-// The 128 x 128 variant (1 wave per SIMD: small problems) uses order 1: at
-// c1 its 32 4-byte DMA issues per wave per K-step were not hidden behind
-// another wave's MFMAs (order 1/3: 0.148 ms per call, order 2: 0.153;
-// tools/experiments/korder_small.sh).  Every order here but 0 is natural,
-// so all variants return the same bits.
+// The small variants (128 x 128 and 128 x 64, 1 wave per SIMD) use order 3:
+// at c1 order 2's 4-byte DMA issues for the query rows (32 per wave per K
+// step) were not hidden behind another wave's MFMAs (round 2, 128 x 128:
+// order 1/3 0.148 ms per call, order 2 0.153); with the 128 x 64 tile order 3
+// (corpus gathered, query 16-byte + swaps) beats order 1: c1 fused kernel
+// 73-74 vs 75-76 us, c2 71 vs 74 (profiles/r3_c1/korder_small_ab.txt).
+// Every order here but 0 is natural, so all variants return the same bits.
 #ifndef PMM_F32_KORDER_SMALL
-#define PMM_F32_KORDER_SMALL 1
+#define PMM_F32_KORDER_SMALL 3
 #endif
 
 template <int NB, int NW, int MODE, int METRIC>
