@@ -699,22 +699,37 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
 // bit the score the main pass gives that (row, column).  Stored S[row][col]
 // (the main pass's candidate buffers, unused until it starts) for
 // seed_select_kernel, which sets gthr[row] = (k-th best composite) - 1: an
-// exact lower bound of the row's final k-th best.  The corpus fragments come
-// straight from global memory (the sample is a few MB, L2-resident); one wave
-// per 32 query rows, one workgroup per 128.  (The first MFMA accumulates onto
-// zeros where the main pass's uses the inline constant 0: the same sums.)
+// exact lower bound of the row's final k-th best.  One wave per 32 query
+// rows, one workgroup per 128; the corpus sample streams through LDS in
+// 32-column blocks (double-buffered, the next block's global loads in flight
+// during this block's MFMAs), staged once per workgroup: round 2 loaded every
+// wave's fragments from global memory, four times the L2 traffic, 1.1 ms at
+// c4 (ns = 1024).  (The first MFMA accumulates onto zeros where the main
+// pass's uses the inline constant 0: the same sums.)
 // ===========================================================================
+template <int KS>
+struct SeedCarve {
+  static constexpr int RB = KS * 256;      // bytes of a sample row's padded K range
+  static constexpr int RS = RB + 16;       // LDS row stride (16 B pad spreads the 32 rows over the banks)
+  static constexpr int CH = RB / 16;       // 16-byte chunks per row
+  static constexpr int NCH = 32 * CH / 256;  // chunks per thread per 32-row block
+  static constexpr int BYTES = 2 * 32 * RS;
+  static_assert((32 * CH) % 256 == 0, "a block's chunks split evenly over 256 threads");
+};
 template <int KS, int METRIC>
 __global__ __launch_bounds__(256, 1) void seed_bf16_ws_kernel(GemmF32Args a, float *__restrict__ S, int ns) {
   using namespace ws;
+  using SC = SeedCarve<KS>;
   constexpr int G = KSUB * KS;  // K substeps of 16
-  const int lane = threadIdx.x & 63;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int r32 = lane & 31, h = lane >> 5;
   const int wrow0 = (int)blockIdx.x * BM + w * 32;
-  if (wrow0 >= a.M) return;  // (wave-uniform)
+  // (wave-uniform; a wave past the last query row still stages and syncs)
+  const bool active = wrow0 < a.M;
   bf16x8 af[G];
-  {
+  if (active) {
     const __amdgpu_buffer_rsrc_t rq =
         make_rsrc(a.qb + (int64_t)wrow0 * a.ldq, (int64_t)min(32, a.M - wrow0) * a.ldq * 2);
     const uint32_t qoff = (uint32_t)(r32 * a.ldq * 2 + 128 * h);
@@ -733,38 +748,72 @@ __global__ __launch_bounds__(256, 1) void seed_bf16_ws_kernel(GemmF32Args a, flo
     qv[e] = (XFORM && row < a.M) ? a.qn[row] : 0.0f;
   }
   const __amdgpu_buffer_rsrc_t rc = make_rsrc(a.cb, (int64_t)ns * a.ldc * 2);
-  for (int t = 0; t < ns / 32; t++) {
-    const int col = t * 32 + r32;
-    // lane (r32, h), substep gs: column col, K-step gs / 8, chunk 8h + gs % 8
-    const uint32_t boff = (uint32_t)(col * a.ldc * 2 + 128 * h);
-    bf16x8 b[G];
+  // block t's rows t*32 .. t*32+31: thread tid carries chunks tid + 256 j
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 pf[SC::NCH];
+  auto fetch = [&](int t) __attribute__((always_inline)) {
 #pragma unroll
-    for (int gs = 0; gs < G; gs++)
-      b[gs] = __builtin_bit_cast(
-          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rc, (int)(boff + ((gs / KSUB) * 128 + (gs % KSUB) * 8) * 2),
-                                                        0, 0));
-    __builtin_amdgcn_sched_barrier(0);  // all of the tile's loads in flight before its MFMAs
-    // the compiler's MFMA builtin (the same instruction as the main pass's
-    // asm, so the same bits): here hipcc allocates the operands freely and
-    // must see the instruction to pad its register hazards
-    typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
-    f32x16 acc = {};
-#pragma unroll
-    for (int gs = 0; gs < G; gs++)
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16v8, af[gs]),
-                                                    __builtin_bit_cast(bf16v8, b[gs]), acc, 0, 0, 0);
-    const float cv = XFORM ? a.cn[col] : 0.0f;
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-      const int row = wrow0 + acc_row(e, h);
-      if (row < a.M) S[(int64_t)row * ns + col] = exact_score<METRIC>(acc[e], qv[e], cv);
+    for (int j = 0; j < SC::NCH; j++) {
+      const int c = tid + 256 * j, r = c / SC::CH, q = c - r * SC::CH;
+      pf[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                            rc, (int)((t * 32 + r) * a.ldc * 2 + q * 16), 0, 0));
     }
+  };
+  auto put = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < SC::NCH; j++) {
+      const int c = tid + 256 * j, r = c / SC::CH, q = c - r * SC::CH;
+      *(u32x4 *)(smem + buf * 32 * SC::RS + r * SC::RS + q * 16) = pf[j];
+    }
+  };
+  const int nt = ns / 32;
+  if (nt > 0) {
+    fetch(0);
+    put(0);
+  }
+  __syncthreads();
+  for (int t = 0; t < nt; t++) {
+    if (t + 1 < nt) fetch(t + 1);
+    if (active) {
+      const int col = t * 32 + r32;
+      // lane (r32, h), substep gs: column col, K-step gs / 8, chunk 8h + gs % 8
+      const char *base = smem + (t & 1) * 32 * SC::RS + r32 * SC::RS + 128 * h;
+      // the compiler's MFMA builtin (the same instruction as the main pass's
+      // asm, so the same bits): here hipcc allocates the operands freely and
+      // must see the instruction to pad its register hazards
+      typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
+      f32x16 acc = {};
+#pragma unroll
+      for (int gs = 0; gs < G; gs++) {
+        const bf16x8 b = *(const bf16x8 *)(base + ((gs / KSUB) * 128 + (gs % KSUB) * 8) * 2);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16v8, af[gs]),
+                                                      __builtin_bit_cast(bf16v8, b), acc, 0, 0, 0);
+      }
+      const float cv = XFORM ? a.cn[col] : 0.0f;
+#pragma unroll
+      for (int e = 0; e < 16; e++) {
+        const int row = wrow0 + acc_row(e, h);
+        if (row < a.M) S[(int64_t)row * ns + col] = exact_score<METRIC>(acc[e], qv[e], cv);
+      }
+    }
+    // block t + 1 into the buffer block t - 1 used (every wave left it at
+    // the previous barrier); visible to all after this one
+    if (t + 1 < nt) put((t + 1) & 1);
+    __syncthreads();
   }
 }
 
 template <int KS, int METRIC>
 static hipError_t launch_seed_bf16_ws_t(const GemmF32Args &a, float *S, int ns, hipStream_t s) {
-  seed_bf16_ws_kernel<KS, METRIC><<<dim3((unsigned)((a.M + ws::BM - 1) / ws::BM)), dim3(256), 0, s>>>(a, S, ns);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void *)seed_bf16_ws_kernel<KS, METRIC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  seed_bf16_ws_kernel<KS, METRIC><<<dim3((unsigned)((a.M + ws::BM - 1) / ws::BM)), dim3(256),
+                                    SeedCarve<KS>::BYTES, s>>>(a, S, ns);
   return hipGetLastError();
 }
 
