@@ -85,12 +85,37 @@ int pmm_set_device(int device);
  * n shards).  Every device runs the fused top-k on its shard with global
  * indices, the per-shard [2][m][k] lists are copied peer to peer (xGMI) to
  * ids[0] and k-way merged there: the result equals the one-device result bit
- * for bit.  A device may be listed more than once (one shard per entry).
- * Process-wide; n = 0 (or ids = NULL) returns to one device.  f64, k > 1024
- * and pmm_matmul_* stay on one device (pmm_set_device's). */
+ * with f32 compute (PMM_COMPUTE_F32): a shard's list is the exact top-k of
+ * its rows under the total order (score, then lower index), so the merged
+ * list equals the one-device result bit for bit.  With PMM_COMPUTE_BF16 the
+ * result is the exact top-k of the bf16-rounded rows up to f32 accumulation
+ * order, as on one device; the shard size can change which bf16 kernel and
+ * threshold seed run, so near-ties may resolve differently than on one device
+ * (tests assert > 99% index agreement).  A device may be listed more than once
+ * (one shard per entry).  A one-entry list moves every host call to that
+ * device.  Work that is not sharded (f64, k > 1024, pmm_matmul_*) runs on
+ * ids[0].  Process-wide; n = 0 (or ids = NULL) returns to one device
+ * (pmm_set_device's).
+ * VERIFIED ON ONE GPU ONLY: the one-GPU test box lists device 0 repeatedly,
+ * which plans all shards onto one stream; the distinct-device branch
+ * (concurrent devices, cross-device event waits, peer copies over xGMI) has
+ * not run on a multi-GPU node yet (tests/test_gpu_parity.py
+ * test_set_devices_distinct_gpus runs it where >= 2 GPUs are visible). */
 int pmm_set_devices(const int *ids, int n);
 /* The current device list: *n entries, the first min(cap, *n) copied to ids. */
 int pmm_get_devices(int *ids, int cap, int *n);
+/* Diagnostics (no reference counterpart; no HIP call, runs without a GPU):
+ * the memory plan the sharded search uses for G shards of an n-row corpus
+ * over devs[0..G-1] (shard g = rows [n g / G, n (g + 1) / G)).  One plan per
+ * DISTINCT device: plan_of[g] = the plan running shard g, *n_plans plans with
+ * plan_dev[j] its device and plan_bytes[j] its device-memory bytes (queries,
+ * host_rows ? uploaded shard rows : nothing, per-shard [2][m][k] lists at
+ * list_offsets[g] inside the plan, one workspace; the root plan, plan_of[0],
+ * also the gathered [G][2][m][k] lists and the merged output).  All output
+ * arrays hold G entries. */
+int pmm_shard_plan(const int *devs, int G, int64_t m, int64_t n, int64_t d, int64_t k, int metric, int compute,
+                   int host_rows, int *plan_of, int *plan_dev, uint64_t *plan_bytes, uint64_t *list_offsets,
+                   int *n_plans);
 
 /* ---------------------------------------------------------------------------
  * Host-buffer entry points (what `_topk` / `_matmul` call; src/lib.rs:15-55).

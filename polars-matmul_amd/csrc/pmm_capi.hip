@@ -1079,6 +1079,79 @@ void enable_peer(int dev, int peer) {
   (void)hipGetLastError();
 }
 
+// Memory plan of topk_sharded (pure: no HIP call, so the CPU tests check it
+// through pmm_shard_plan).  One DevPlan per DISTINCT device of the list: that
+// device's queries once, one workspace (its shards run in stream order), and
+// per shard the uploaded rows (host shards only) and its [2][m][k] list; the
+// root plan (the first shard's device) also holds the gathered [G][2][m][k]
+// lists and the merged output.
+struct DevPlan {
+  int dev;
+  hipStream_t s = nullptr;
+  char *base = nullptr;
+  size_t off_q = 0, off_qb = 0, off_ws = 0, ws_bytes = 0, total = 0;
+};
+struct ShardLayout {
+  std::vector<DevPlan> dps;
+  std::vector<int> plan_of;  // shard -> index into dps
+  std::vector<size_t> off_c, off_cb, off_list;
+  size_t off_gather = 0, off_out = 0;  // in the root plan
+};
+
+int device_cus(int dev) {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  return (dev >= 0 && dev < kMaxDevices && g_dev[dev].probed) ? g_dev[dev].cus : 256;
+}
+
+void plan_sharded(const std::vector<ShardSrc> &sh, int64_t m, int64_t d, int64_t k, int metric, int compute,
+                  ShardLayout &L) {
+  const int G = (int)sh.size();
+  const bool bf16 = compute == PMM_COMPUTE_BF16;
+  const int64_t dp = bf16 ? cdiv(d, kBf16DAlign) * kBf16DAlign : cdiv(d, 32) * 32;
+  const size_t list_bytes = (size_t)2 * m * k * 4;
+  L.dps.clear();
+  L.plan_of.assign(G, 0);
+  L.off_c.assign(G, 0);
+  L.off_cb.assign(G, 0);
+  L.off_list.assign(G, 0);
+  for (int g = 0; g < G; g++) {
+    int j = 0;
+    while (j < (int)L.dps.size() && L.dps[j].dev != sh[g].dev) j++;
+    if (j == (int)L.dps.size()) {
+      DevPlan p;
+      p.dev = sh[g].dev;
+      L.dps.push_back(p);
+    }
+    L.plan_of[g] = j;
+  }
+  for (auto &p : L.dps) {
+    size_t off = 0;
+    p.off_q = off;  // f32: padded rows; bf16: f32 staging rows (stride d)
+    off = al256(off + (size_t)m * (bf16 ? d : dp) * 4);
+    p.off_qb = off;  // bf16 rows
+    off = al256(off + (bf16 ? (size_t)m * dp * 2 : 0));
+    for (int g = 0; g < G; g++) {
+      if (sh[g].dev != p.dev) continue;
+      Plan tp;
+      plan_topk(m, sh[g].rows, dp, k, metric, device_cus(p.dev), tp, compute);
+      p.ws_bytes = std::max(p.ws_bytes, tp.total);
+      L.off_c[g] = off;
+      if (sh[g].host) off = al256(off + (size_t)sh[g].rows * (bf16 ? d : dp) * 4);
+      L.off_cb[g] = off;
+      if (bf16) off = al256(off + (size_t)sh[g].rows * dp * 2);
+      L.off_list[g] = off;
+      off = al256(off + list_bytes);
+    }
+    p.off_ws = off;
+    off = al256(off + p.ws_bytes);
+    p.total = off;
+  }
+  DevPlan &rp = L.dps[L.plan_of[0]];
+  L.off_gather = rp.total;
+  L.off_out = al256(L.off_gather + (size_t)G * list_bytes);
+  rp.total = al256(L.off_out + list_bytes);
+}
+
 int topk_sharded(const float *q, int64_t m, int64_t d, int64_t k, int metric, int compute,
                  const std::vector<ShardSrc> &sh, uint32_t *out_idx, float *out_score) {
   const int G = (int)sh.size();
@@ -1092,53 +1165,15 @@ int topk_sharded(const float *q, int64_t m, int64_t d, int64_t k, int metric, in
   const int64_t dp = bf16 ? cdiv(d, kBf16DAlign) * kBf16DAlign : cdiv(d, 32) * 32;
   const int root = sh[0].dev;
   const size_t list_bytes = (size_t)2 * m * k * 4;
-  // per distinct device: the queries once, one workspace (its shards run in
-  // stream order), per shard the uploaded rows (host shards) and its list
-  struct DevPlan {
-    int dev;
-    hipStream_t s = nullptr;
-    char *base = nullptr;
-    size_t off_q = 0, off_qb = 0, off_ws = 0, ws_bytes = 0, total = 0;
-  };
-  std::vector<DevPlan> dps;
-  std::vector<int> plan_of(G);
-  std::vector<size_t> off_c(G), off_cb(G), off_list(G);
-  for (int g = 0; g < G; g++) {
-    int j = 0;
-    while (j < (int)dps.size() && dps[j].dev != sh[g].dev) j++;
-    if (j == (int)dps.size()) {
-      if (int rc = probe_device(sh[g].dev)) return rc;
-      DevPlan p;
-      p.dev = sh[g].dev;
-      dps.push_back(p);
-    }
-    plan_of[g] = j;
-  }
-  for (auto &p : dps) {
-    HIP_TRY(hipSetDevice(p.dev));
-    size_t off = 0;
-    p.off_q = off;  // f32: padded rows; bf16: f32 staging rows (stride d)
-    off = al256(off + (size_t)m * (bf16 ? d : dp) * 4);
-    p.off_qb = off;  // bf16 rows
-    off = al256(off + (bf16 ? (size_t)m * dp * 2 : 0));
-    for (int g = 0; g < G; g++) {
-      if (sh[g].dev != p.dev) continue;
-      p.ws_bytes = std::max(p.ws_bytes, pmm_topk_workspace_bytes(m, sh[g].rows, dp, k, metric, compute));
-      off_c[g] = off;
-      if (sh[g].host) off = al256(off + (size_t)sh[g].rows * (bf16 ? d : dp) * 4);
-      off_cb[g] = off;
-      if (bf16) off = al256(off + (size_t)sh[g].rows * dp * 2);
-      off_list[g] = off;
-      off = al256(off + list_bytes);
-    }
-    p.off_ws = off;
-    off = al256(off + p.ws_bytes);
-    p.total = off;
-  }
-  // root: the gathered lists and the merged output
+  for (const ShardSrc &x : sh)
+    if (int rc = probe_device(x.dev)) return rc;
+  ShardLayout L;
+  plan_sharded(sh, m, d, k, metric, compute, L);
+  std::vector<DevPlan> &dps = L.dps;
+  const std::vector<int> &plan_of = L.plan_of;
+  const std::vector<size_t> &off_c = L.off_c, &off_cb = L.off_cb, &off_list = L.off_list;
   DevPlan &rp = dps[plan_of[0]];
-  const size_t off_gather = rp.total, off_out = al256(off_gather + (size_t)G * list_bytes);
-  rp.total = al256(off_out + list_bytes);
+  const size_t off_gather = L.off_gather, off_out = L.off_out;
   for (auto &p : dps) {
     HIP_TRY(hipSetDevice(p.dev));
     if (int rc = thread_stream(p.dev, &p.s)) return rc;
@@ -1249,6 +1284,16 @@ std::vector<int> devices_snapshot() {
   return g_devs;
 }
 
+// The device host entry points run on when a device list is set: its first
+// entry (the root, which also merges a sharded search), else -1 (the thread's
+// pmm_set_device choice or the current device).  A one-entry list therefore
+// moves all host work to that device; work that is not sharded (f64, k > 1024,
+// .pmm.matmul) runs on the root of a longer list.
+int list_root() {
+  std::lock_guard<std::mutex> lk(g_devs_mu);
+  return g_devs.empty() ? -1 : g_devs[0];
+}
+
 // shard g of n rows over G shards: rows [n g / G, n (g + 1) / G)
 int64_t shard_lo(int64_t n, int G, int g) { return n * g / G; }
 
@@ -1304,7 +1349,7 @@ int pmm_device_memory(size_t *free_bytes, size_t *total_bytes) {
   if (!free_bytes || !total_bytes) return fail(PMM_ERR_ARG, "null argument");
   int dev, rc;
   DevScope scope;
-  if ((rc = ensure_device(&dev, &scope))) return rc;
+  if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
   HIP_TRY(hipMemGetInfo(free_bytes, total_bytes));
   return PMM_OK;
 }
@@ -1342,6 +1387,34 @@ int pmm_set_devices(const int *ids, int n) {
     if (int rc = probe_device(ids[i])) return rc;
   std::lock_guard<std::mutex> lk(g_devs_mu);
   g_devs.assign(ids, ids + n);
+  return PMM_OK;
+}
+
+int pmm_shard_plan(const int *devs, int G, int64_t m, int64_t n, int64_t d, int64_t k, int metric, int compute,
+                   int host_rows, int *plan_of, int *plan_dev, uint64_t *plan_bytes, uint64_t *list_offsets,
+                   int *n_plans) {
+  if (!devs || G < 1 || !plan_of || !plan_dev || !plan_bytes || !list_offsets || !n_plans)
+    return fail(PMM_ERR_ARG, "null argument or empty device list");
+  if (m < 1 || n < G || d < 1 || k < 1 || k > kFusedMaxK)
+    return fail(PMM_ERR_ARG, "bad sizes (m=%lld n=%lld G=%d d=%lld k=%lld)", (long long)m, (long long)n, G,
+                (long long)d, (long long)k);
+  static const float kHostTag = 0.0f;  // any non-null host pointer: rows are uploaded
+  std::vector<ShardSrc> sh(G);
+  for (int g = 0; g < G; g++) {
+    const int64_t lo = shard_lo(n, G, g), hi = shard_lo(n, G, g + 1);
+    sh[g] = ShardSrc{devs[g], lo, hi - lo, host_rows ? &kHostTag : nullptr, nullptr, nullptr};
+  }
+  ShardLayout L;
+  plan_sharded(sh, m, d, k, metric, compute, L);
+  *n_plans = (int)L.dps.size();
+  for (int j = 0; j < (int)L.dps.size(); j++) {
+    plan_dev[j] = L.dps[j].dev;
+    plan_bytes[j] = L.dps[j].total;
+  }
+  for (int g = 0; g < G; g++) {
+    plan_of[g] = L.plan_of[g];
+    list_offsets[g] = L.off_list[g];
+  }
   return PMM_OK;
 }
 
@@ -1461,7 +1534,7 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
   }
   int dev;
   DevScope scope;
-  if ((rc = ensure_device(&dev, &scope))) return rc;
+  if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   if (compute == PMM_COMPUTE_BF16) {
@@ -1552,7 +1625,7 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
   int dev;
   DevScope scope;
-  if ((rc = ensure_device(&dev, &scope))) return rc;
+  if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   const int64_t dp = cdiv(d, 16) * 16;
@@ -1614,7 +1687,7 @@ int pmm_matmul_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t
   if (m == 0 || n == 0) return PMM_OK;
   int dev;
   DevScope scope;
-  if ((rc = ensure_device(&dev, &scope))) return rc;
+  if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   const int64_t dp = cdiv(std::max<int64_t>(d, 1), 32) * 32;
@@ -1648,7 +1721,7 @@ int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64
   if (m == 0 || n == 0) return PMM_OK;
   int dev;
   DevScope scope;
-  if ((rc = ensure_device(&dev, &scope))) return rc;
+  if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   const int64_t dp = cdiv(std::max<int64_t>(d, 1), 16) * 16;
@@ -1747,7 +1820,7 @@ int pmm_corpus_create_f32(const float *c, int64_t n, int64_t d, pmm_corpus **out
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
   int dev;
   DevScope scope;
-  if ((rc = ensure_device(&dev, &scope))) return rc;
+  if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
   std::vector<int> devs = devices_snapshot();
   if (devs.size() <= 1) devs.assign(1, dev);
   const int G = (int)std::min<int64_t>((int64_t)devs.size(), n);

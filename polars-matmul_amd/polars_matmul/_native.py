@@ -10,6 +10,7 @@ RuntimeError with the library's message.
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import importlib.util
 import os
@@ -47,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "pmm_set_device",
     "pmm_set_devices",
     "pmm_get_devices",
+    "pmm_shard_plan",
     "pmm_topk_f32",
     "pmm_topk_f32_ex",
     "pmm_topk_f64",
@@ -119,6 +121,10 @@ _SIGS = {
     "pmm_set_device": ([_i32], _i32),
     "pmm_set_devices": ([ctypes.POINTER(ctypes.c_int), _i32], _i32),
     "pmm_get_devices": ([ctypes.POINTER(ctypes.c_int), _i32, ctypes.POINTER(ctypes.c_int)], _i32),
+    "pmm_shard_plan": ([ctypes.POINTER(ctypes.c_int), _i32, _i64, _i64, _i64, _i64, _i32, _i32, _i32,
+                        ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                        ctypes.POINTER(ctypes.c_int)], _i32),
     "pmm_topk_f32": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_topk_f32_ex": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _i32, _vp, _vp], _i32),
     "pmm_topk_f64": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
@@ -221,6 +227,22 @@ def get_devices():
     return list(arr[:n.value])
 
 
+def shard_plan(devs, m: int, n: int, d: int, k: int, metric: int, compute: int = COMPUTE_F32,
+               host_rows: bool = True):
+    """The sharded search's memory plan (pmm_shard_plan; pure, no GPU):
+    (plan_of[g], [(device, bytes) per distinct-device plan], list_offsets[g])."""
+    G = len(devs)
+    arr = (ctypes.c_int * G)(*[int(x) for x in devs])
+    plan_of = (ctypes.c_int * G)()
+    plan_dev = (ctypes.c_int * G)()
+    plan_bytes = (ctypes.c_uint64 * G)()
+    offs = (ctypes.c_uint64 * G)()
+    npl = ctypes.c_int(0)
+    check(_lib.pmm_shard_plan(arr, G, m, n, d, k, metric, compute, 1 if host_rows else 0, plan_of, plan_dev,
+                              plan_bytes, offs, ctypes.byref(npl)))
+    return (list(plan_of), [(plan_dev[j], int(plan_bytes[j])) for j in range(npl.value)], [int(x) for x in offs])
+
+
 def metric_from_str(s: str) -> int:
     out = ctypes.c_int(-1)
     check(_lib.pmm_metric_from_str(s.encode(), ctypes.byref(out)))
@@ -264,7 +286,15 @@ class PinnedPool:
     rate, and the buffer becomes the Arrow child buffer of the result Series
     without a copy.  Blocks come back when their arrays are freed; at most
     `cap_bytes` of idle blocks are kept (PMM_PINNED_POOL_BYTES, default 1 GiB;
-    0 disables the pool)."""
+    0 disables the pool).
+
+    Re-entrancy: a block's finaliser can run inside any allocation (a cyclic
+    GC pass), including one made by `take` on the same thread.  So returning a
+    block takes no lock and allocates nothing: `_give_back` appends
+    (ptr, nbytes) to a deque (append is atomic), and `take` moves returned
+    blocks into the free lists under the lock, where nothing is allocated
+    either (the lists are preallocated per size; Python objects for the result
+    are built after the lock is released)."""
 
     MIN_BYTES = 1 << 20  # smaller results: a plain numpy array
 
@@ -273,34 +303,61 @@ class PinnedPool:
         self.free = {}  # nbytes -> [ptr, ...]
         self.idle = 0
         self.lock = threading.Lock()
+        self.returned = collections.deque()  # (ptr, nbytes) from finalisers, lock-free
+
+    def _absorb(self):
+        """Move finalised blocks into the free lists (lock held by caller).
+        Returns the pointers that exceed the cap, to be freed after the lock
+        is released."""
+        over = []
+        while True:
+            try:
+                p, nbytes = self.returned.popleft()
+            except IndexError:
+                return over
+            if self.idle + nbytes <= self.cap:
+                self.free.setdefault(nbytes, []).append(p)
+                self.idle += nbytes
+            else:
+                over.append(p)
 
     def take(self, nbytes: int):
         """A (pointer, owner) for nbytes, or None (pool off, too small, or the
         allocation failed)."""
         if self.cap <= 0 or nbytes < self.MIN_BYTES:
             return None
+        p = None
         with self.lock:
+            over = self._absorb()
             lst = self.free.get(nbytes)
             if lst:
                 self.idle -= nbytes
                 p = lst.pop()
-                return p, _PinnedBlock(p, nbytes, self)
-        out = ctypes.c_void_p()
-        if _lib.pmm_host_alloc(nbytes, ctypes.byref(out)) != PMM_OK or not out.value:
-            return None
-        return out.value, _PinnedBlock(out.value, nbytes, self)
+        for q in over:
+            _lib.pmm_host_free(q)
+        if p is None:
+            out = ctypes.c_void_p()
+            if _lib.pmm_host_alloc(nbytes, ctypes.byref(out)) != PMM_OK or not out.value:
+                return None
+            p = out.value
+        return p, _PinnedBlock(p, nbytes, self)
 
     def _give_back(self, p: int, nbytes: int) -> None:
+        # runs from finalisers: no lock, no allocation beyond the deque node
+        self.returned.append((p, nbytes))
+
+    def idle_bytes(self) -> int:
         with self.lock:
-            if self.idle + nbytes <= self.cap:
-                self.free.setdefault(nbytes, []).append(p)
-                self.idle += nbytes
-                return
-        _lib.pmm_host_free(p)
+            over = self._absorb()
+            n = self.idle
+        for q in over:
+            _lib.pmm_host_free(q)
+        return n
 
     def clear(self) -> None:
         with self.lock:
-            ptrs = [p for lst in self.free.values() for p in lst]
+            over = self._absorb()
+            ptrs = [p for lst in self.free.values() for p in lst] + over
             self.free.clear()
             self.idle = 0
         for p in ptrs:

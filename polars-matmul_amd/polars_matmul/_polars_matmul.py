@@ -348,8 +348,10 @@ def _topk(left, right, k, metric):
         sc = np.zeros((m, 0), dtype=np.float64)
     else:
         _apply_devices_env()
-        # (a device-sharded handle serves k <= 1024; larger k runs on one GPU)
-        dc = _cached_corpus(right, rv, c) if use_f32 and (kk <= 1024 or not _native.get_devices()) else None
+        # (a handle sharded over several GPUs serves k <= 1024; larger k runs
+        # on one GPU, the device list's first)
+        dc = (_cached_corpus(right, rv, c)
+              if use_f32 and (kk <= 1024 or len(_native.get_devices()) <= 1) else None)
         if dc is not None:
             try:
                 idx, sc = dc.topk(q, kk, metric_id)

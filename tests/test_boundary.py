@@ -372,15 +372,48 @@ def test_pinned_pool_recycles_blocks_and_falls_back(monkeypatch):
     p = a.ctypes.data
     del a
     gc.collect()
-    assert pool.idle == 0 and float(arr[5].as_py()) == 3.0
+    assert pool.idle_bytes() == 0 and float(arr[5].as_py()) == 3.0
     del arr
     gc.collect()
-    assert pool.idle == 4 << 20  # back in the pool
+    assert pool.idle_bytes() == 4 << 20  # back in the pool
     b = _native.pinned_empty((1024, 1024), np.float32)
-    assert b.ctypes.data == p and pool.idle == 0  # recycled, not reallocated
+    assert b.ctypes.data == p and pool.idle_bytes() == 0  # recycled, not reallocated
     small = _native.pinned_empty((4, 4), np.float32)  # below MIN_BYTES: plain numpy
     assert small.base is None or not hasattr(small.base, "_pmm_block")
     del b
     gc.collect()
     pool.clear()
     assert frees == [p]
+
+
+def test_pinned_pool_finaliser_inside_take_does_not_deadlock(monkeypatch):
+    # a block finalised by a GC pass that starts inside `take`
+    # (on the same thread, while the pool works) must not wait on the pool's
+    # lock.  Simulate it: the stub allocator drops the last reference to a
+    # live block while `take` runs; with a lock taken in the finaliser this
+    # would hang.
+    store = {}
+    pending = []
+
+    class StubLib:
+        def pmm_host_alloc(self, nbytes, out):
+            pending.clear()  # finalises the held block right here
+            b = ctypes.create_string_buffer(nbytes)
+            store[ctypes.addressof(b)] = b
+            out._obj.value = ctypes.addressof(b)
+            return 0
+
+        def pmm_host_free(self, p):
+            return 0
+
+    monkeypatch.setattr(_native, "_lib", StubLib())
+    pool = _native.PinnedPool(64 << 20)
+    got = pool.take(2 << 20)
+    pending.append(got[1])
+    del got
+    with pool.lock:  # finaliser runs while the lock is held: must not block
+        pending.clear()
+    pending.append(pool.take(2 << 20)[1])  # reuses the returned block, no alloc
+    t = pool.take(3 << 20)  # allocates; the stub finalises the 2 MiB block inside
+    assert t is not None
+    assert pool.idle_bytes() == 2 << 20

@@ -966,6 +966,62 @@ def test_set_devices_through_extension_and_cache(pmm, device_list):
         pm.clear_corpus_cache()
 
 
+def test_set_devices_one_entry_runs_there(pmm, device_list):
+    # a one-entry list is not ignored -- host calls run on that
+    # device (device 0 is the only one on the one-GPU box; the plan is the
+    # one-device plan) and corpus handles are created there, unsharded
+    n = device_list
+    rs = np.random.RandomState(13)
+    q = rs.randn(50, 96).astype(np.float32)
+    c = rs.randn(3000, 96).astype(np.float32)
+    want = n.topk_host(q, c, 20, METRICS["cosine"])
+    n.set_devices([0])
+    assert n.get_devices() == [0]
+    got = n.topk_host(q, c, 20, METRICS["cosine"])
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    dc = n.DeviceCorpus(c)
+    assert dc.shards == 1
+    assert np.array_equal(dc.topk(q, 1500, METRICS["dot"])[0], n.topk_host(q, c, 1500, METRICS["dot"])[0])
+    dc.close()
+
+
+def _visible_gpus():
+    try:
+        return _native().device_count()
+    except Exception:
+        return 0
+
+
+needs_2gpu = pytest.mark.skipif(_visible_gpus() < 2, reason="needs >= 2 visible GPUs (distinct-device branch)")
+
+
+@needs_2gpu
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_set_devices_distinct_gpus(pmm, device_list, metric):
+    # the distinct-device branch of topk_sharded -- one DevPlan per
+    # device, concurrent launches, cross-device event waits, peer copies into
+    # the root -- bit-equal to one GPU, through host top-k and a sharded
+    # corpus handle, and with the root on another device than the first
+    n = device_list
+    G = min(4, n.device_count())
+    rs = np.random.RandomState(31)
+    q = rs.randn(400, 256).astype(np.float32)
+    c = rs.randn(60011, 256).astype(np.float32)
+    c[-50:] = c[:50]  # ties across shard boundaries
+    want = n.topk_host(q, c, 100, METRICS[metric])
+    n.set_devices(list(range(G)))
+    got = n.topk_host(q, c, 100, METRICS[metric])
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1].view(np.uint32), want[1].view(np.uint32))
+    dc = n.DeviceCorpus(c)
+    assert dc.shards == G
+    got = dc.topk(q, 100, METRICS[metric])
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1].view(np.uint32), want[1].view(np.uint32))
+    dc.close()
+    n.set_devices(list(reversed(range(G))))  # root on the last device
+    got = n.topk_host(q, c, 100, METRICS[metric])
+    assert np.array_equal(got[0], want[0])
+
+
 # ---- the 256-row bf16 kernel (pmm_bf16_dsx_kernel.h; lab build only: `make
 # lab`, PMM_LIB=libpmm_lab.so, PMM_BF16_DSX=1, padded D 256 / 512 / 768)
 # against the wave-specialised kernel and float64 truth ----
