@@ -161,16 +161,22 @@ def ref_inputs(M, N, D):
 
 
 def load_traffic(config: str):
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    --pmc summary (profiles/), corrected as MI355X_MICROARCH.md prescribes."""
+    """(HBM bytes per launch of the dominant kernel, its source record) from
+    the committed rocprofv3 --pmc summary of this build (profiles/
+    pmc_traffic_<config>.json, written by tools/traffic_json.py), corrected as
+    MI355X_MICROARCH.md prescribes."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            rec = json.load(f)
+        return rec.get("hbm_bytes_per_launch"), {
+            "source": rec.get("source"), "traffic_over_algorithmic": rec.get("traffic_over_algorithmic"),
+            "algorithmic_bytes_per_launch": rec.get("algorithmic_bytes_per_launch"),
+            "l2_hit_rate": rec.get("l2_hit_rate")}
     except Exception:
-        return None
+        return None, None
 
 
 # ---------------------------------------------------------------------------
@@ -191,6 +197,38 @@ def cpu_oracle_qps(q, c, k, metric, threads, reps=1, warm=0):
         ts.append(time.perf_counter() - t0)
     dt = float(np.median(ts))
     return q.shape[0] / dt, dt
+
+
+def cpu_blas_qps(q, c, k, metric, threads, reps=1, warm=0):
+    """the reference's structure with a BLAS-class GEMM
+    (oracle.topk_blas: ndarray-order norms, OpenBLAS sgemm through NumPy on
+    `threads` threads in the role of faer's Parallelism::Rayon(0)
+    (src/metrics.rs:244-251) into the M x N matrix, then the oracle's
+    single-threaded epilogue and per-row select).  Median seconds of `reps`
+    calls and the phase split of the median call."""
+    import oracle
+
+    mid = oracle.metric_from_str(metric)
+    for _ in range(warm):
+        oracle.topk_blas(q, c, k, mid, nthreads=threads)
+    runs = []
+    for _ in range(reps):
+        ph = {}
+        t0 = time.perf_counter()
+        oracle.topk_blas(q, c, k, mid, nthreads=threads, timings=ph)
+        runs.append((time.perf_counter() - t0, ph))
+    runs.sort(key=lambda r: r[0])
+    dt, ph = runs[len(runs) // 2]
+    return q.shape[0] / dt, dt, {kk: round(v * 1000.0, 2) for kk, v in ph.items()}
+
+
+def blas_name() -> str:
+    try:
+        cfg = np.show_config(mode="dicts")
+        b = cfg["Build Dependencies"]["blas"]
+        return f"{b.get('name', 'blas')} {b.get('version', '')}".strip()
+    except Exception:
+        return "NumPy BLAS"
 
 
 def numpy_comparator(q, c, k, reps=1, warm=0):
@@ -271,6 +309,7 @@ def matmul_line(args, reps=20, warm=3):
         "note": "result bytes M*N*4 = 40 MB per call, copied into a pooled page-locked block: the "
                 "PCIe copy, not the GEMM, bounds the call",
     }
+    line["sweep"] = matmul_sweep(cpu=bool(args.cpu_sample))
     if args.cpu_sample:
         for _ in range(2):
             qh @ ch.T
@@ -289,10 +328,23 @@ def matmul_line(args, reps=20, warm=3):
     return line
 
 
-def boundary_rates(q_dev, c_dev, k, metric_id, compute=0):
+def _median_time(fn, reps, warm):
+    for _ in range(warm):
+        fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def boundary_rates(q_dev, c_dev, k, metric_id, compute=0, reps=5, warm=1):
     """Host-boundary rates: host f32 buffers in, host idx/score
-    out, through the C ABI, one call each (untimed by the contract's clock):
-      host_api: pmm_topk_f32 -- pins, uploads Q and C, computes, downloads;
+    out, through the C ABI, median of `reps` calls after `warm` full-size
+    warm-ups (untimed by the contract's clock):
+      host_api: pmm_topk_f32 -- uploads Q and C (pageable host memory; the
+        corpus in chunks overlapped with compute), computes, downloads;
       cached_corpus: pmm_topk_f32_corpus -- corpus resident (uploaded once,
         as the Arrow-keyed cache does across map_batches calls), Q uploaded
         and results downloaded per call."""
@@ -301,22 +353,177 @@ def boundary_rates(q_dev, c_dev, k, metric_id, compute=0):
     qh = q_dev.cpu().numpy()
     ch = c_dev.cpu().numpy()
     M = qh.shape[0]
-    out = {}
+    out = {"reps": reps, "warmup": warm}
     _native.topk_host(qh[:1024], ch[:4096], k, metric_id, compute=compute)  # first-call setup
-    t0 = time.perf_counter()
-    _native.topk_host(qh, ch, k, metric_id, compute=compute)
-    out["host_api_qps"] = round(M / (time.perf_counter() - t0), 2)
+    dt, ts = _median_time(lambda: _native.topk_host(qh, ch, k, metric_id, compute=compute), reps, warm)
+    out["host_api_qps"] = round(M / dt, 2)
+    out["host_api_s"] = [round(t, 4) for t in ts]
     if compute != _native.COMPUTE_F32:
         return out  # the corpus handle is f32-only
     t0 = time.perf_counter()
     dc = _native.DeviceCorpus(ch)
     out["corpus_upload_s"] = round(time.perf_counter() - t0, 3)
     dc.topk(qh[:1024], k, metric_id)  # first-call allocations
-    t0 = time.perf_counter()
-    dc.topk(qh, k, metric_id)
-    out["cached_corpus_qps"] = round(M / (time.perf_counter() - t0), 2)
+    dt, ts = _median_time(lambda: dc.topk(qh, k, metric_id), reps, warm)
+    out["cached_corpus_qps"] = round(M / dt, 2)
+    out["cached_corpus_s"] = [round(t, 4) for t in ts]
     dc.close()
     return out
+
+
+# ---------------------------------------------------------------------------
+# The reference's own benchmarks, end to end through the extension surface
+# 
+# ---------------------------------------------------------------------------
+def _arrow_rows(a, fixed):
+    """a's rows as a Polars List[f] column's Arrow form (LargeList) or as an
+    Array[f, d] (FixedSizeList) -- what `.cast(pl.List(..))` / `pl.Array`
+    hand the plugin (benchmark_topk.py:76-82, benchmark_matmul.py:54-60)."""
+    import pyarrow as pa
+
+    m, d = a.shape
+    vals = pa.array(a.reshape(-1))
+    if fixed:
+        return pa.FixedSizeListArray.from_arrays(vals, d)
+    return pa.LargeListArray.from_arrays(pa.array(np.arange(m + 1, dtype=np.int64) * d), vals)
+
+
+def _explode_unnest(res, qid):
+    """`.explode("m").unnest("m")` of benchmark_topk.py:56-60 on Arrow: the
+    query id repeated per hit, the index and score columns."""
+    import pyarrow.compute as pc
+
+    parents = pc.list_parent_indices(res)
+    flat = res.flatten()
+    return qid.take(parents), flat.field("index"), flat.field("score")
+
+
+def _native_split():
+    """(h2d, kernels, d2h) ms of the library's event records since the last reset."""
+    from polars_matmul import _native
+
+    tot, _ = _native.timing_read("")
+    h2d, _ = _native.timing_read("h2d")
+    d2h, _ = _native.timing_read("d2h")
+    return h2d, tot - h2d - d2h, d2h
+
+
+def e2e_topk_line(reps=5, warm=2):
+    """benchmark_topk.py:48-64 / :79-91 at its base size (BASELINE configs[0]/
+    [1] shape: 1000 x 10000 x 256, k = 10, cosine, seed-42 inputs): the whole
+    `.pmm.topk` call (`_topk` on the Arrow form of a Polars List[f32] column,
+    then explode + unnest), median of `reps` after `warm` warm-ups, as the
+    reference times it.  Legs: List and Array (FixedSizeList) inputs, f32 and
+    f64 (the reference's "Varying Dtype"); `cached` = repeated calls with the
+    same corpus column (the device corpus cache hits after the first call),
+    `first_call` = the cache cleared before each call (corpus uploaded and its
+    norms computed every time).  Per leg the median call's split: extract
+    (Arrow -> contiguous matrices), h2d / kernels / d2h (HIP events of the
+    library), device_other (host time in the C-ABI call outside the events'
+    span: staging, launch, sync), assemble (f64 widening + Arrow List[Struct])
+    and explode_unnest."""
+    import pyarrow as pa
+
+    from polars_matmul import _native
+    from polars_matmul import _polars_matmul as pm
+
+    M, N, D, k, metric = CONFIGS["c1"][:5]
+    qid = pa.array(np.arange(M, dtype=np.int64))
+    out = {"workload": f"{M}x{N}x{D} {metric} k={k}, seed-42 inputs (benchmark_topk.py:69-71)",
+           "reps": reps, "warmup": warm}
+    for dt_name, dtype in (("f32", np.float32), ("f64", np.float64)):
+        np.random.seed(42)
+        qh = np.random.randn(M, D).astype(dtype)
+        ch = np.random.randn(N, D).astype(dtype)
+        for fixed in (False, True):
+            qa, ca = _arrow_rows(qh, fixed), _arrow_rows(ch, fixed)
+            legs = ("cached", "first_call") if dtype == np.float32 else ("cached",)
+            for leg in legs:
+                def call():
+                    if leg == "first_call":
+                        pm.clear_corpus_cache()
+                    res = pm._topk(qa, ca, k, metric)
+                    _explode_unnest(res, qid)
+
+                for _ in range(warm):
+                    call()
+                runs = []
+                for _ in range(reps):
+                    ph = {}
+                    pm.PHASES = ph
+                    _native.timing_reset()
+                    _native.timing_enable(True)
+                    t0 = time.perf_counter()
+                    res = None
+                    if leg == "first_call":
+                        pm.clear_corpus_cache()
+                    t1 = time.perf_counter()
+                    res = pm._topk(qa, ca, k, metric)
+                    t2 = time.perf_counter()
+                    _explode_unnest(res, qid)
+                    t3 = time.perf_counter()
+                    _native.timing_enable(False)
+                    pm.PHASES = None
+                    h2d, kern, d2h = _native_split()
+                    ph["explode_unnest"] = t3 - t2
+                    runs.append((t3 - t1, t0, ph, h2d, kern, d2h))
+                runs.sort(key=lambda r: r[0])
+                tot, _, ph, h2d, kern, d2h = runs[len(runs) // 2]
+                name = f"{dt_name}_{'array' if fixed else 'list'}_{leg}"
+                dev_ms = ph.get("device", 0.0) * 1000.0
+                out[name] = {
+                    "ms_per_call": round(tot * 1000.0, 3), "queries_per_s": round(M / tot, 1),
+                    "all_ms": sorted(round(r[0] * 1000.0, 3) for r in runs),
+                    "split_ms": {"extract": round(ph.get("extract", 0.0) * 1000.0, 3),
+                                 "h2d": round(h2d, 3), "kernels": round(kern, 3), "d2h": round(d2h, 3),
+                                 "device_other": round(max(0.0, dev_ms - h2d - kern - d2h), 3),
+                                 "assemble": round(ph.get("assemble", 0.0) * 1000.0, 3),
+                                 "explode_unnest": round(ph.get("explode_unnest", 0.0) * 1000.0, 3)},
+                }
+                log(f"e2e {name}: {out[name]}")
+        pm.clear_corpus_cache()
+    # the README's figure for the reference on its (unstated) hardware
+    out["reference_readme_ms"] = 45.0
+    return out
+
+
+def matmul_sweep(reps=10, warm=3, cpu=True):
+    """benchmark_matmul.py:110-143: `.pmm.matmul` (`_matmul` on the Arrow form
+    of the columns) over its points -- queries 500/1000/2000, corpus
+    5000/10000/20000, dim 128/256/512 around 1000 x 10000 x 256, f32 and f64,
+    Array and List inputs -- median of `reps` calls after `warm` warm-ups, as
+    the reference times it (:33-41), with NumPy's BLAS product (np.dot, :23-30)
+    on this host beside it."""
+    from polars_matmul import _polars_matmul as pm
+
+    base = (1000, 10000, 256)
+    pts = []
+    for qq in (500, 1000, 2000):
+        pts.append((qq, base[1], base[2], "f32", "array"))
+    for cc in (5000, 20000):
+        pts.append((base[0], cc, base[2], "f32", "array"))
+    for dd in (128, 512):
+        pts.append((base[0], base[1], dd, "f32", "array"))
+    pts.append((*base, "f64", "array"))
+    pts.append((*base, "f32", "list"))
+    pts.append((*base, "f64", "list"))
+    rows = []
+    for (m, n, d, dt_name, kind) in pts:
+        dtype = np.float32 if dt_name == "f32" else np.float64
+        np.random.seed(42)
+        qh = np.random.randn(m, d).astype(dtype)
+        ch = np.random.randn(n, d).astype(dtype)
+        qa, ca = _arrow_rows(qh, kind == "array"), _arrow_rows(ch, kind == "array")
+        t, _ = _median_time(lambda: pm._matmul(qa, ca), reps, warm)
+        row = {"queries": m, "corpus": n, "dim": d, "dtype": dt_name, "input": kind,
+               "pmm_ms": round(t * 1000.0, 3)}
+        if cpu:
+            tn, _ = _median_time(lambda: np.dot(qh, ch.T), reps, warm)
+            row["numpy_ms"] = round(tn * 1000.0, 3)
+            row["ratio"] = round(t / tn, 3)
+        rows.append(row)
+        log(f"matmul sweep {row}")
+    return rows
 
 
 # ---------------------------------------------------------------------------
@@ -483,6 +690,7 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8, stride=1)
         check = spot_check(q, c, lo, k, metric, out_i, out_s, rows, dist, world, rank)
     flops = 2.0 * M * n_loc * D
     peak = MFMA_PEAK_TFLOPS[cdt]
+    traffic, traffic_rec = load_traffic(name) if world == 1 else (None, None)
     gemm_ms, _ = ks["gemm"]
     seed_ms, _ = ks["seed"]
     all_gemm_ms = (gemm_ms or 0.0) + (seed_ms or 0.0)
@@ -495,7 +703,8 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8, stride=1)
         "achieved": round(ach, 2) if ach else None,
         "peak": peak, "unit": "TFLOP/s",
         "frac": round(ach / peak, 4) if ach else None,
-        "traffic": load_traffic(name) if world == 1 else None,
+        "traffic": traffic,
+        "traffic_record": traffic_rec,
         # per launch of the dominant kernel; a threshold-seeding pass
         # (small problems only) is its own launch of the same
         # kernel and is counted in "achieved"/"frac" too
@@ -578,6 +787,84 @@ def cpu_selftest(args, rank, world):
         dist.destroy_process_group()
 
 
+def inproc_child(args) -> None:
+    """the drop-in boundary's own multi-GPU transport, in ONE
+    fresh process (started by rank 0 after the RCCL ranks are done, before
+    anything here touches the GPU): pmm_set_devices(0..N-1), a corpus handle
+    row-sharded over the N devices at creation (pmm_corpus_create_f32), then
+    pmm_topk_f32_corpus per step -- host queries uploaded to every device,
+    every device's fused top-k concurrently, the [2][M][k] lists copied peer
+    to peer into device 0 and merged there, results downloaded.  Prints one
+    JSON line."""
+    import torch
+    from polars_matmul import _native
+
+    n = args.inproc_child
+    M, N, D, k, metric, cdt = CONFIGS[args.config]
+    if cdt != "f32":
+        print(json.dumps({"error": "in-process transport measured for f32 configs only"}), flush=True)
+        return
+    mid = _native.metric_from_str(metric)
+    dev0 = torch.device("cuda", 0)
+    # the same rows bench.py's ranks generate, brought to the host
+    qh = synth_rows(0, M, D, QSEED, dev0).cpu().numpy()
+    ch = synth_rows(0, N, D, CSEED, dev0).cpu().numpy()
+    torch.cuda.empty_cache()
+    # (rehearsal on a one-GPU box: PMM_BENCH_INPROC_DEVICES=0,0 lists device 0 twice)
+    devs = os.environ.get("PMM_BENCH_INPROC_DEVICES")
+    _native.set_devices([int(x) for x in devs.split(",")] if devs else list(range(n)))
+    t0 = time.perf_counter()
+    dc = _native.DeviceCorpus(ch)
+    up = time.perf_counter() - t0
+    del ch
+    steps, warm = max(1, min(args.steps, 5)), max(1, min(args.warmup, 1))
+    for _ in range(warm):
+        dc.topk(qh, k, mid)
+    _native.timing_reset()
+    _native.timing_enable(True)
+    ts = []
+    for _ in range(steps):
+        t1 = time.perf_counter()
+        out_i, _ = dc.topk(qh, k, mid)
+        ts.append(time.perf_counter() - t1)
+    _native.timing_enable(False)
+    gms, gn = _native.timing_read("gemm_f32_topk")
+    mms, mn = _native.timing_read("merge_devices")
+    h2d, hn = _native.timing_read("h2d")
+    dt = float(np.median(ts))
+    print(json.dumps({
+        "transport": "in-process (pmm_set_devices + sharded corpus handle; peer copies into device 0)",
+        "n_gpus": n, "devices": _native.get_devices(), "shards": dc.shards, "workload": f"{M}x{N}x{D} {cdt} {metric} k={k} ({args.config})",
+        "value": round(M / dt, 2), "unit": "queries/s", "ms_per_call": round(dt * 1000.0, 3),
+        "steps": steps, "warmup": warm, "all_ms": [round(t * 1000.0, 3) for t in ts],
+        "shard_kernel_ms_avg": round(gms / gn, 3) if gn else None, "shard_kernel_launches": gn,
+        "root_merge_ms_avg": round(mms / mn, 3) if mn else None,
+        "h2d_ms_per_call": round(h2d / steps, 3) if hn else None,
+        "corpus_upload_s": round(up, 3),
+        "note": "host queries in, host lists out (the .pmm.topk boundary): the H2D of the queries to every "
+                "device and the D2H of the merged lists are inside the call",
+    }), flush=True)
+    dc.close()
+
+
+def run_inproc_child(args, world):
+    """Start the in-process transport measurement as a fresh child process
+    (no torch.distributed env) and return its JSON record."""
+    env = {kk: v for kk, v in os.environ.items()
+           if kk not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                         "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID")}
+    cmd = [sys.executable, os.path.abspath(__file__), "--inproc-child", str(world), "--config", args.config,
+           "--steps", str(args.steps), "--warmup", str(args.warmup)]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.inproc_timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"in-process child timed out after {args.inproc_timeout} s"}
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"in-process child rc={r.returncode}", "stderr_tail": r.stderr[-800:]}
+    return json.loads(lines[-1])
+
+
 def extra_line(name, steps, warmup, dev, args):
     """Secondary workload on this GPU (N = 1 runs only), reported under
     "extra"; the reference-size configs also carry their CPU baselines timed
@@ -594,16 +881,29 @@ def extra_line(name, steps, warmup, dev, args):
         # lists of the same rows (the main line's c3 output, same inputs)
         fields["check"]["recall_at_k_vs_f32_all_rows"] = round(recall_at_k(lists, ref), 6)
     del lists
+    if name == "c1":
+        # the reference's own benchmark, end to end through `_topk` on Arrow
+        # List / Array columns (host buffers in, Arrow List[Struct] out)
+        fields["boundary"] = e2e_topk_line()
     if name in REF_INPUT_CONFIGS and args.cpu_sample:
         k, metric = CONFIGS[name][3], CONFIGS[name][4]
         qh, ch = ref_inputs(M, N, D)
-        qps, dt = cpu_oracle_qps(qh, ch, k, metric, args.cpu_threads, reps=5, warm=2)
+        qps, dt, ph = cpu_blas_qps(qh, ch, k, metric, args.cpu_threads, reps=5, warm=2)
         fields["cpu_baseline"] = {
             "value": round(qps, 2), "unit": "queries/s", "cores": args.cpu_threads,
             "host_nproc": os.cpu_count(), "available_parallelism": available_parallelism(), "kind": "port",
+            "gemm": f"{blas_name()} sgemm via NumPy, {args.cpu_threads} threads (faer Rayon(0)'s role)",
             "sample": f"the full {M}x{N}x{D} {metric} k={k} workload (seed-42 inputs, "
-                      f"benchmark_topk.py:69-71), median of 5 after 2 warm-ups: {dt * 1000:.1f} ms; "
-                      "oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select)",
+                      f"benchmark_topk.py:69-71), median of 5 after 2 warm-ups: {dt * 1000:.1f} ms; the "
+                      "reference's structure (norms, threaded BLAS GEMM, 1-thread epilogue + per-row select; "
+                      "oracle.topk_blas)",
+            "phases_ms": ph,
+        }
+        oqps, odt = cpu_oracle_qps(qh, ch, k, metric, args.cpu_threads, reps=5, warm=2)
+        fields["cpu_baseline_oracle_loop"] = {
+            "value": round(oqps, 2), "unit": "queries/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"full workload, median of 5 after 2 warm-ups: {odt * 1000:.1f} ms; oracle/pmm_oracle.c "
+                      "with its own scalar-blocked GEMM (the checker)",
         }
         if metric == "cosine":
             nq, ndt = numpy_comparator(qh, ch, k, reps=5, warm=2)
@@ -638,7 +938,15 @@ def main():
                     help="record the per-kernel HIP events on every n-th timed step (0: every step of "
                          "a run of at most 20 steps, every 50th of a longer one)")
     ap.add_argument("--cpu-selftest", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--inproc", type=int, default=1,
+                    help="N > 1: after the RCCL ranks, also measure the in-process transport (one child "
+                         "process driving all N GPUs through pmm_set_devices) under extra.inproc")
+    ap.add_argument("--inproc-timeout", type=int, default=900, help=argparse.SUPPRESS)
+    ap.add_argument("--inproc-child", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.inproc_child:
+        inproc_child(args)
+        return
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # this process only launches: no torch.cuda / HIP call happens here
@@ -686,18 +994,27 @@ def main():
                                   _native.COMPUTE_BF16 if cdt == "bf16" else _native.COMPUTE_F32)
         log(f"boundary: {boundary}")
 
-    cpu = cpu_np = None
+    cpu = cpu_np = cpu_oracle = None
     if args.cpu_sample and world == 1 and rank == 0:
         n_s = min(args.cpu_sample, M)
         qh = q[:n_s].float().cpu().numpy()
         ch = c.float().cpu().numpy()
-        # bf16: the oracle on the bf16-rounded rows (widened to f32, exact)
-        cpu_qps, cpu_dt = cpu_oracle_qps(qh, ch, k, metric, args.cpu_threads)
+        # bf16: the baselines on the bf16-rounded rows (widened to f32, exact)
+        cpu_qps, cpu_dt, cpu_ph = cpu_blas_qps(qh, ch, k, metric, args.cpu_threads)
         cpu = {
             "value": round(cpu_qps, 2), "unit": "queries/s", "cores": args.cpu_threads,
             "host_nproc": os.cpu_count(), "available_parallelism": available_parallelism(), "kind": "port",
-            "sample": f"first {n_s} queries x full {N}-row corpus, {D}d {cdt} {metric} k={k}; "
-                      f"oracle/pmm_oracle.c (threaded GEMM, 1-thread epilogue+select), {cpu_dt:.1f}s",
+            "gemm": f"{blas_name()} sgemm via NumPy, {args.cpu_threads} threads (faer Rayon(0)'s role)",
+            "sample": f"first {n_s} queries x full {N}-row corpus, {D}d {cdt} {metric} k={k}; the reference's "
+                      f"structure (matmul.rs:420-469): norms, threaded BLAS GEMM into the M x N matrix, "
+                      f"1-thread epilogue + per-row select (oracle.topk_blas), {cpu_dt:.1f}s",
+            "phases_ms": cpu_ph,
+        }
+        o_qps, o_dt = cpu_oracle_qps(qh[:min(n_s, 128)], ch, k, metric, args.cpu_threads)
+        cpu_oracle = {
+            "value": round(o_qps, 2), "unit": "queries/s", "cores": args.cpu_threads, "kind": "port",
+            "sample": f"first {min(n_s, 128)} queries x full corpus; oracle/pmm_oracle.c's own scalar-blocked "
+                      f"GEMM (the checker's k-ordered chain), {o_dt:.1f}s",
         }
         if metric == "cosine":
             np_qps, np_dt = numpy_comparator(qh, ch, k)
@@ -722,8 +1039,20 @@ def main():
 
     if rank != 0:
         if dist:
+            dist.barrier()
             dist.destroy_process_group()
         return
+    inproc = None
+    if world > 1:
+        dist.barrier()  # the other ranks leave after this barrier
+    if world > 1 and args.inproc:
+        # the RCCL measurement is complete on every rank; free this rank's
+        # device memory and let the other ranks exit, then one fresh process
+        # drives all N GPUs through the drop-in boundary
+        del q, c
+        torch.cuda.empty_cache()
+        inproc = run_inproc_child(args, world)
+        log(f"inproc: {inproc}")
 
     line = {
         "metric": "cosine top-k queries/sec",
@@ -746,8 +1075,9 @@ def main():
         "reduction_roofline": fields["reduction_roofline"],
         "cpu_baseline": cpu,
         "cpu_baseline_numpy": cpu_np,
+        "cpu_baseline_oracle_loop": cpu_oracle,
         "boundary": boundary,
-        "extra": extra,
+        "extra": extra if inproc is None else dict(extra or {}, inproc=inproc),
         "check": fields["check"],
     }
     print(json.dumps(line), flush=True)

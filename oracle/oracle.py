@@ -15,6 +15,15 @@ Every function restates a reference function (paths into the reference tree):
 * ``matmul``           -> src/metrics.rs:40-255 (dst = Q * C^T)
 * ``pair_scores``      -> the element S[i, idx[i, j]] of ``similarity`` (f32),
                           without materialising S (full-size parity checks)
+* ``topk_blas``        -> src/matmul.rs:420-469 with the reference's STRUCTURE
+                          for timing: ndarray-order norms, a threaded BLAS GEMM
+                          (OpenBLAS sgemm/dgemm through NumPy in the role of
+                          faer's Parallelism::Rayon(0), src/metrics.rs:244-251)
+                          into the materialised M x N matrix, then the
+                          single-threaded epilogue (:314-365) and per-row
+                          select (src/topk.rs:42-75).  The CPU baseline that
+                          bench.py times; not the checker (BLAS blocking order
+                          differs from the oracle's k-ordered chain).
 """
 from __future__ import annotations
 
@@ -63,6 +72,8 @@ def lib():
         L.oracle_topk_f64.argtypes = [vp, i64, vp, i64, i64, i64, i32, i32, vp, vp]
         L.oracle_topk_f64.restype = i64
         L.oracle_pair_scores_f32.argtypes = [vp, i64, vp, i64, i64, i32, vp, i64, i32, vp]
+        L.oracle_epilogue_f32.argtypes = [vp, i64, i64, i32, vp, vp]
+        L.oracle_epilogue_f64.argtypes = [vp, i64, i64, i32, vp, vp]
         _lib = L
     return _lib
 
@@ -144,3 +155,42 @@ def pair_scores(q: np.ndarray, c: np.ndarray, idx: np.ndarray, metric: int, nthr
     lib().oracle_pair_scores_f32(_p(q), m, _p(c), c.shape[0], q.shape[1], metric, _p(idx), k,
                                  nthreads, _p(out))
     return out
+
+
+def topk_blas(q: np.ndarray, c: np.ndarray, k: int, metric: int, nthreads: int = 0, timings: dict = None):
+    """The reference's topk structure with a BLAS-class threaded GEMM (see the
+    module docstring).  Returns (idx uint32 [M,k'], scores float64 [M,k']);
+    `timings`, if given, receives the seconds of each phase (norms, gemm,
+    epilogue, select)."""
+    import time
+
+    dt = np.float32 if (q.dtype == np.float32 and c.dtype == np.float32) else np.float64
+    q, c = _as(q, dt), _as(c, dt)
+    m, d = q.shape
+    n = c.shape[0]
+    kk = min(k, n)
+    L = lib()
+    t0 = time.perf_counter()
+    qn = cn = None
+    if metric != DOT:
+        qn = norms(q, squared=metric == EUCLIDEAN)
+        cn = norms(c, squared=metric == EUCLIDEAN)
+    t1 = time.perf_counter()
+    if nthreads > 0:
+        from threadpoolctl import threadpool_limits
+
+        with threadpool_limits(limits=nthreads, user_api="blas"):
+            s = q @ c.T
+    else:
+        s = q @ c.T
+    s = np.ascontiguousarray(s)
+    t2 = time.perf_counter()
+    if metric != DOT:
+        fn = L.oracle_epilogue_f32 if dt == np.float32 else L.oracle_epilogue_f64
+        fn(_p(s), m, n, metric, _p(qn), _p(cn))
+    t3 = time.perf_counter()
+    idx, sc = select_topk(s, kk, metric != EUCLIDEAN)
+    t4 = time.perf_counter()
+    if timings is not None:
+        timings.update(norms=t1 - t0, gemm=t2 - t1, epilogue=t3 - t2, select=t4 - t3)
+    return idx, sc.astype(np.float64)

@@ -920,6 +920,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
 int upload_padded(void *dst, const void *src, int64_t rows, int64_t d, int64_t dp, size_t elem,
                   hipStream_t s) {
   if (rows <= 0) return PMM_OK;
+  Timed t("h2d", s);  // bench.py's end-to-end breakdown (pmm_timing_*)
   if (dp == d) {
     HIP_TRY(hipMemcpyAsync(dst, src, (size_t)rows * d * elem, hipMemcpyHostToDevice, s));
   } else {
@@ -1035,8 +1036,11 @@ int topk_f32_host_chunked(const float *q, int64_t m, const float *c, int64_t n, 
     Timed t("merge_chunks", s);
     CHUNK_TRY(launch_merge(ma, 1, s));
   }
-  CHUNK_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
-  CHUNK_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  {
+    Timed t("d2h", s);
+    CHUNK_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+    CHUNK_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  }
   CHUNK_TRY(hipStreamSynchronize(s));
 #undef CHUNK_TRY
   return finish(PMM_OK);
@@ -1556,8 +1560,11 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
                                db, n, d, k, metric, 0u, (uint32_t *)(b + off_i),
                                (float *)(b + off_s), b + off_w, ws_need, s, dev);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+    {
+      Timed t("d2h", s);
+      HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+    }
     HIP_TRY(hipStreamSynchronize(s));
     return PMM_OK;
   }
@@ -1579,8 +1586,11 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
                             d, k, metric, 0u, (uint32_t *)(b + off_i), (float *)(b + off_s),
                             b + off_w, ws_need, s, dev);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  {
+    Timed t("d2h", s);
+    HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  }
   HIP_TRY(hipStreamSynchronize(s));
   return PMM_OK;
 }
@@ -1675,8 +1685,11 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
                                     (int)k, 0u, oi + r0 * k, os + r0 * k, s));
     }
   }
-  HIP_TRY(hipMemcpyAsync(out_idx, oi, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(out_score, os, (size_t)m * k * 8, hipMemcpyDeviceToHost, s));
+  {
+    Timed t("d2h", s);
+    HIP_TRY(hipMemcpyAsync(out_idx, oi, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_score, os, (size_t)m * k * 8, hipMemcpyDeviceToHost, s));
+  }
   HIP_TRY(hipStreamSynchronize(s));
   return PMM_OK;
 }
@@ -1936,8 +1949,11 @@ int pmm_topk_f32_corpus(const pmm_corpus *h, const float *q, int64_t m, int64_t 
                             0u, (uint32_t *)(b + off_i), (float *)(b + off_s), b + off_w, ws_need,
                             s, dev, shard_norms(x));
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  {
+    Timed t("d2h", s);
+    HIP_TRY(hipMemcpyAsync(out_idx, b + off_i, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_score, b + off_s, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+  }
   HIP_TRY(hipStreamSynchronize(s));
   return PMM_OK;
 }

@@ -29,6 +29,7 @@ from __future__ import annotations
 import collections
 import os
 import threading
+import time
 
 import numpy as np
 import pyarrow as pa
@@ -40,6 +41,21 @@ try:  # Polars is optional: the HIP path does not need it.
     import polars as _pl  # type: ignore
 except Exception:  # pragma: no cover - polars is not installed in this image
     _pl = None
+
+
+# Host-side phase timer for bench.py's end-to-end breakdown: when set to a
+# dict, _topk / _matmul add the seconds of each phase (extract: Arrow/numpy ->
+# contiguous matrices; device: the C-ABI call -- upload, kernels, download;
+# assemble: result dtype widening and Arrow assembly).  None (default): off.
+PHASES = None
+
+
+def _lap(name: str, t0: float) -> float:
+    t = time.perf_counter()
+    ph = PHASES
+    if ph is not None:
+        ph[name] = ph.get(name, 0.0) + (t - t0)
+    return t
 
 
 class PanicException(BaseException):
@@ -326,6 +342,7 @@ def _topk(left, right, k, metric):
     if not isinstance(metric, str):
         raise TypeError(f"argument 'metric': '{type(metric).__name__}' object cannot be converted to 'PyString'")
     polars_out = _is_polars_series(left)
+    t = time.perf_counter()
     lv = _to_arrow(left)
     rv = _to_arrow(right)
     if _nrows(lv) == 0:  # src/matmul.rs:480-487
@@ -339,6 +356,7 @@ def _topk(left, right, k, metric):
     dt = np.float32 if use_f32 else np.float64
     q = _series_to_matrix(lv, dt)
     c = _series_to_matrix(rv, dt)
+    t = _lap("extract", t)
     if q.shape[1] != c.shape[1]:  # src/matmul.rs:433-441
         raise _dim_mismatch(q.shape[1], c.shape[1])
     kk = min(k, c.shape[0])  # src/matmul.rs:443
@@ -359,13 +377,17 @@ def _topk(left, right, k, metric):
                 dc.release()
         else:
             idx, sc = _native.topk_host(q, c, kk, metric_id)
+        t = _lap("device", t)
         sc = sc.astype(np.float64, copy=False)  # src/matmul.rs:447 (f32 -> f64)
-    return _wrap(_topk_arrow(idx, sc, m, kk), "topk", polars_out)
+    out = _wrap(_topk_arrow(idx, sc, m, kk), "topk", polars_out)
+    _lap("assemble", t)
+    return out
 
 
 def _matmul(left, right):
     """src/lib.rs:15-30 -> src/matmul.rs:295-417 matmul_impl."""
     polars_out = _is_polars_series(left)
+    t = time.perf_counter()
     lv = _to_arrow(left)
     rv = _to_arrow(right)
     use_f32 = _is_f32(lv) and _is_f32(rv)  # src/matmul.rs:298, :308
@@ -375,12 +397,16 @@ def _matmul(left, right):
         return _wrap(pa.array([], type=pa.large_list(pa_t)), "matmul", polars_out)
     q = _series_to_matrix(lv, dt)
     c = _series_to_matrix(rv, dt)
+    t = _lap("extract", t)
     if q.shape[1] != c.shape[1]:
         raise _dim_mismatch(q.shape[1], c.shape[1])
     out = _native.matmul_host(q, c)
+    t = _lap("device", t)
     n = c.shape[0]
     arr = pa.FixedSizeListArray.from_arrays(pa.array(out.reshape(-1), type=pa_t), n)
-    return _wrap(arr, "matmul", polars_out)
+    res = _wrap(arr, "matmul", polars_out)
+    _lap("assemble", t)
+    return res
 
 
 __all__ = ["_matmul", "_topk", "PanicException", "clear_corpus_cache", "set_devices", "get_devices"]
