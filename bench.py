@@ -787,6 +787,75 @@ def cpu_selftest(args, rank, world):
         dist.destroy_process_group()
 
 
+F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X FP64 matrix, AMD spec (MI355X_MICROARCH.md lists no f64 row)
+
+
+def f64_line(steps=200, warmup=10):
+    """the f64 top-k (what Polars' default Float64 columns
+    take; src/matmul.rs:449-468) at the reference benchmark's size, c1 inputs
+    as f64 (seed 42, cosine, k = 10), resident in HBM: pmm_topk_f64_device per
+    step, fused (default) and materialised (PMM_F64_FUSED=0) alternately timed;
+    the GEMM launches' roofline against the f64 MFMA peak."""
+    import torch
+    from polars_matmul import _native
+
+    M, N, D, k, metric = CONFIGS["c1"][:5]
+    mid = _native.metric_from_str(metric)
+    qh, ch = ref_inputs(M, N, D)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    q = torch.from_numpy(qh.astype(np.float64)).to(dev)
+    c = torch.from_numpy(ch.astype(np.float64)).to(dev)
+    oi = torch.empty((M, k), dtype=torch.int32, device=dev)
+    os_ = torch.empty((M, k), dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def run():
+        _native.topk_f64_device(q.data_ptr(), D, M, c.data_ptr(), D, N, D, k, mid, oi.data_ptr(), os_.data_ptr(),
+                                stream=stream)
+
+    out = {"workload": f"{M}x{N}x{D} f64 {metric} k={k} (c1 inputs as f64)", "dtype": "f64"}
+    for mode in ("fused", "materialised"):
+        if mode == "materialised":
+            os.environ["PMM_F64_FUSED"] = "0"
+        try:
+            for _ in range(warmup):
+                run()
+            torch.cuda.synchronize()
+            _native.timing_reset()
+            _native.timing_enable(True)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                run()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            _native.timing_enable(False)
+        finally:
+            os.environ.pop("PMM_F64_FUSED", None)
+        gname = "gemm_f64_topk" if mode == "fused" else "gemm_f64_scores"
+        gms, gn = _native.timing_read(gname)
+        tot, tn = _native.timing_read("")
+        ach = 2.0 * M * N * D / (gms / steps / 1000.0) / 1e12 if gn else None
+        rec = {"value": round(M * steps / el, 2), "unit": "queries/s", "ms_per_step": round(el / steps * 1000.0, 4),
+               "steps": steps, "warmup": warmup, "gemm_ms_per_step": round(gms / steps, 4) if gn else None,
+               "gemm_launches_per_step": gn // steps if gn else None,
+               "kernels_ms_per_step": round(tot / steps, 4) if tn else None}
+        if ach:
+            rec["roofline"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": F64_MFMA_PEAK_TFLOPS,
+                               "unit": "TFLOP/s", "frac": round(ach / F64_MFMA_PEAK_TFLOPS, 4),
+                               "peak_source": "AMD spec (FP64 matrix); not in MI355X_MICROARCH.md"}
+        out[mode] = rec
+        log(f"f64 {mode}: {rec}")
+    # exactness of this run's lists against the oracle (first 64 rows)
+    import oracle
+
+    got = oi.cpu().numpy().view(np.uint32)
+    oi_, _ = oracle.topk(qh[:64].astype(np.float64), ch.astype(np.float64), k, oracle.metric_from_str(metric))
+    out["check"] = {"rows": 64, "exact_index_match_frac": float(np.mean(got[:64] == oi_))}
+    del q, c
+    torch.cuda.empty_cache()
+    return out
+
+
 def inproc_child(args) -> None:
     """the drop-in boundary's own multi-GPU transport, in ONE
     fresh process (started by rank 0 after the RCCL ranks are done, before
@@ -930,9 +999,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="oracle baseline threads (0 = available_parallelism(), as faer's Rayon(0))")
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
-    ap.add_argument("--extra", default="c4,c1,c2,matmul",
+    ap.add_argument("--extra", default="c4,c1,c2,c1_f64,matmul",
                     help="comma-separated secondary configs measured after the main line (N=1; 'none' = none; "
-                         "'matmul' = .pmm.matmul at the c1 size)")
+                         "'matmul' = .pmm.matmul at the c1 size; 'c1_f64' = the f64 top-k at the c1 size)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 top-k")
     ap.add_argument("--timing-stride", type=int, default=0,
                     help="record the per-kernel HIP events on every n-th timed step (0: every step of "
@@ -1033,8 +1102,8 @@ def main():
         torch.cuda.empty_cache()
         extra = {}
         for name in [x for x in args.extra.split(",") if x and x not in (args.config, "none")]:
-            extra[name] = extra_line(name, args.steps, args.warmup, dev, args) if name != "matmul" \
-                else matmul_line(args)
+            extra[name] = (matmul_line(args) if name == "matmul" else f64_line() if name == "c1_f64"
+                           else extra_line(name, args.steps, args.warmup, dev, args))
             log(f"extra {name}: {json.dumps(extra[name])}")
 
     if rank != 0:

@@ -142,6 +142,18 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
 int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t d, int64_t k,
                  int metric, uint32_t *out_idx, double *out_score);
 
+/* The same f64 top-k on device rows (row strides >= roundup(d, 16), zero-
+ * padded, 16-byte-aligned bases) on the caller's stream; out_idx / out_score
+ * are device buffers of m*k entries, indices offset by index_base.  k <=
+ * 1024: fused (f64 MFMA GEMM whose epilogue appends each element that beats
+ * its row's running k-th to a candidate buffer, the corpus scanned in growing
+ * column chunks with the k-th raised between chunks: no m x n matrix), else
+ * (or when a row's buffer overflows) the materialised GEMM + row select.
+ * Synchronises the stream before returning (the overflow check). */
+int pmm_topk_f64_device(const double *q, int64_t ldq, int64_t m, const double *c, int64_t ldc, int64_t n,
+                        int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *out_idx,
+                        double *out_score, void *stream);
+
 /* Replaces matmul_slice_f32 / matmul_f32 (src/metrics.rs:160-202, :204-255):
  * out (m x n, row-major) = Q * C^T. */
 int pmm_matmul_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d, float *out);

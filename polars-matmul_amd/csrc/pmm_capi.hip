@@ -1283,6 +1283,184 @@ int topk_sharded(const float *q, int64_t m, int64_t d, int64_t k, int metric, in
   return finish(PMM_OK);
 }
 
+// ---------------------------------------------------------------------------
+// f64 top-k (src/matmul.rs:449-468 -> src/metrics.rs:258-311 + src/topk.rs:6-39)
+// on device rows of stride >= roundup(d, 16), zero-padded.  k <= kFusedMaxK:
+// the fused chunked scan of pmm_f64.hip (no M x N matrix); a row whose buffer
+// overflowed (adversarial data: every chunk beats the last) or k above the
+// fused limit: the materialised path (f64 GEMM store + row select), which also
+// serves as the PMM_F64_FUSED=0 reference.
+// ---------------------------------------------------------------------------
+struct F64Plan {
+  int cap = 0, P = 0;
+  int64_t mc = 0;  // query rows per pass (candidate-buffer budget)
+  size_t off_qn = 0, off_cn = 0, off_tkey = 0, off_tidx = 0, off_cnt = 0, off_cand = 0, off_flag = 0,
+         off_mat = 0, total = 0;
+};
+constexpr size_t kF64CandBudget = size_t(1) << 30;
+
+void plan_f64(int64_t m, int64_t n, int64_t k, F64Plan &p) {
+  p.cap = std::min(4096, std::max(1024, next_pow2(4 * (int)std::min<int64_t>(k, kFusedMaxK) + 256)));
+  p.P = p.cap;
+  p.mc = std::max<int64_t>(1, std::min<int64_t>(m, (int64_t)(kF64CandBudget / ((size_t)p.cap * 16))));
+  size_t off = 0;
+  p.off_flag = off;
+  off += 256;
+  p.off_qn = off;
+  off = al256(off + (size_t)m * 8);
+  p.off_cn = off;
+  off = al256(off + (size_t)n * 8);
+  p.off_tkey = off;
+  off = al256(off + (size_t)p.mc * 8);
+  p.off_tidx = off;
+  off = al256(off + (size_t)p.mc * 4);
+  p.off_cnt = off;
+  off = al256(off + (size_t)p.mc * 4);
+  p.off_cand = off;
+  off = al256(off + (size_t)p.mc * p.cap * 16);
+  p.total = off;
+}
+
+size_t f64_workspace_bytes(int64_t m, int64_t n, int64_t k, int metric) {
+  (void)metric;
+  F64Plan p;
+  plan_f64(m, n, k, p);
+  MatPlan mp;
+  plan_materialise(m, n, k, 8, mp);
+  return std::max(p.total, mp.total);
+}
+
+bool f64_fused_enabled() {
+  const char *e = getenv("PMM_F64_FUSED");  // read per call (tests compare both paths)
+  return !(e && atoi(e) == 0);
+}
+
+int topk_f64_materialised(const double *dq, int64_t ldq, int64_t m, const double *dc, int64_t ldc, int64_t n,
+                          int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *oi, double *os,
+                          char *w, hipStream_t s) {
+  MatPlan p;
+  plan_materialise(m, n, k, 8, p);
+  double *qn = (double *)(w + p.off_qn), *cn = (double *)(w + p.off_cn);
+  double *sc = (double *)(w + p.off_scores);
+  if (metric != kMetricDot) {
+    const int sq = metric == kMetricEuclidean;
+    HIP_TRY(launch_norms_f64(dq, m, d, ldq, sq, qn, s));
+    HIP_TRY(launch_norms_f64(dc, n, d, ldc, sq, cn, s));
+  }
+  const int64_t dp = cdiv(d, 16) * 16;
+  for (int64_t r0 = 0; r0 < m; r0 += p.rows) {
+    const int64_t rows = std::min<int64_t>(p.rows, m - r0);
+    {
+      Timed t("gemm_f64_scores", s);
+      HIP_TRY(launch_gemm_f64_store(dq + r0 * ldq, ldq, dc, ldc, qn + r0, cn, (int)rows, (int)n, (int)dp, metric,
+                                    1, sc, n, s));
+    }
+    if (!p.global_sort) {
+      RowSelArgs ra{};
+      ra.scores = sc;
+      ra.lds = n;
+      ra.rows = (int)rows;
+      ra.N = (int)n;
+      ra.k = (int)k;
+      ra.P = p.P;
+      ra.metric = metric;
+      ra.is_f64 = 1;
+      ra.index_base = index_base;
+      ra.out_idx = oi + r0 * k;
+      ra.out_score = os + r0 * k;
+      Timed t("select_f64_rows", s);
+      HIP_TRY(launch_rowselect(ra, s));
+    } else {
+      HIP_TRY(launch_rowsort_global(sc, n, (int)rows, (int)n, 1, metric, w + p.off_keys, p.P2, (int)k, index_base,
+                                    oi + r0 * k, os + r0 * k, s));
+    }
+  }
+  return PMM_OK;
+}
+
+int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double *dc, int64_t ldc, int64_t n,
+                         int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *oi, double *os, char *w,
+                         hipStream_t s) {
+  if (k > kFusedMaxK || !f64_fused_enabled())
+    return topk_f64_materialised(dq, ldq, m, dc, ldc, n, d, k, metric, index_base, oi, os, w, s);
+  F64Plan p;
+  plan_f64(m, n, k, p);
+  const int64_t dp = cdiv(d, 16) * 16;
+  double *qn = (double *)(w + p.off_qn), *cn = (double *)(w + p.off_cn);
+  unsigned *flag = (unsigned *)(w + p.off_flag);
+  if (metric != kMetricDot) {
+    const int sq = metric == kMetricEuclidean;
+    Timed t("norms_f64", s);
+    HIP_TRY(launch_norms_f64(dq, m, d, ldq, sq, qn, s));
+    HIP_TRY(launch_norms_f64(dc, n, d, ldc, sq, cn, s));
+  }
+  // chunk schedule: the first chunk fills half a buffer (accept-all), later
+  // chunks are g times the columns seen, about g*k survivors per row each
+  const int64_t s0 = std::min<int64_t>(n, p.cap / 2);
+  const int64_t g = std::max<int64_t>(1, (p.cap / 2 - k) / std::max<int64_t>(k, 1));
+  HIP_TRY(hipMemsetAsync(flag, 0, 4, s));
+  for (int64_t r0 = 0; r0 < m; r0 += p.mc) {
+    const int rows = (int)std::min<int64_t>(p.mc, m - r0);
+    unsigned long long *tkey = (unsigned long long *)(w + p.off_tkey);
+    uint32_t *tidx = (uint32_t *)(w + p.off_tidx);
+    unsigned *cnt = (unsigned *)(w + p.off_cnt);
+    Ent *cand = (Ent *)(w + p.off_cand);
+    HIP_TRY(launch_f64_reset(tkey, tidx, cnt, rows, flag + 1, s));
+    F64TopkArgs a{};
+    a.q = dq + r0 * ldq;
+    a.c = dc;
+    a.qn = qn + r0;
+    a.cn = cn;
+    a.ldq = ldq;
+    a.ldc = ldc;
+    a.M = rows;
+    a.D = (int)dp;
+    a.metric = metric;
+    a.tkey = tkey;
+    a.tidx = tidx;
+    a.cnt = cnt;
+    a.cand = cand;
+    a.cap = p.cap;
+    F64SelArgs sa{};
+    sa.cand = cand;
+    sa.cnt = cnt;
+    sa.cap = p.cap;
+    sa.M = rows;
+    sa.k = (int)k;
+    sa.P = p.P;
+    sa.tkey = tkey;
+    sa.tidx = tidx;
+    sa.metric = metric;
+    sa.index_base = index_base;
+    sa.out_idx = oi + r0 * k;
+    sa.out_score = os + r0 * k;
+    sa.overflow = flag;
+    int64_t seen = 0, chunk = s0;
+    while (seen < n) {
+      const int64_t cc = std::min<int64_t>(chunk, n - seen);
+      a.col0 = (int)seen;
+      a.ncol = (int)cc;
+      {
+        Timed t("gemm_f64_topk", s);
+        HIP_TRY(launch_gemm_f64_topk(a, s));
+      }
+      seen += cc;
+      sa.mode = seen < n ? 0 : 1;
+      {
+        Timed t("select_f64", s);
+        HIP_TRY(launch_f64_select(sa, s));
+      }
+      chunk = seen * g;
+    }
+  }
+  // an overflowed row dropped candidates: redo the call on the materialised path
+  unsigned of = 0;
+  HIP_TRY(hipMemcpyAsync(&of, flag, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (of) return topk_f64_materialised(dq, ldq, m, dc, ldc, n, d, k, metric, index_base, oi, os, w, s);
+  return PMM_OK;
+}
+
 std::vector<int> devices_snapshot() {
   std::lock_guard<std::mutex> lk(g_devs_mu);
   return g_devs;
@@ -1639,52 +1817,17 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
   hipStream_t s;
   if ((rc = thread_stream(dev, &s))) return rc;
   const int64_t dp = cdiv(d, 16) * 16;
-  MatPlan p;
-  plan_materialise(m, n, k, 8, p);
   size_t off_q = 0, off_c = al256((size_t)m * dp * 8), off_i = off_c + al256((size_t)n * dp * 8);
   size_t off_s = off_i + al256((size_t)m * k * 4), off_w = off_s + al256((size_t)m * k * 8);
   void *base;
-  if ((rc = arena(dev, s, off_w + p.total, &base))) return rc;
+  if ((rc = arena(dev, s, off_w + f64_workspace_bytes(m, n, k, metric), &base))) return rc;
   char *b = (char *)base;
-  char *w = b + off_w;
   const double *dq = (const double *)(b + off_q), *dc = (const double *)(b + off_c);
   if ((rc = upload_padded(b + off_q, q, m, d, dp, 8, s))) return rc;
   if ((rc = upload_padded(b + off_c, c, n, d, dp, 8, s))) return rc;
-  double *qn = (double *)(w + p.off_qn), *cn = (double *)(w + p.off_cn);
-  double *sc = (double *)(w + p.off_scores);
-  if (metric != kMetricDot) {
-    const int sq = metric == kMetricEuclidean;
-    HIP_TRY(launch_norms_f64(dq, m, d, dp, sq, qn, s));
-    HIP_TRY(launch_norms_f64(dc, n, d, dp, sq, cn, s));
-  }
   uint32_t *oi = (uint32_t *)(b + off_i);
   double *os = (double *)(b + off_s);
-  for (int64_t r0 = 0; r0 < m; r0 += p.rows) {
-    const int64_t rows = std::min<int64_t>(p.rows, m - r0);
-    {
-      Timed t("gemm_f64_scores", s);
-      HIP_TRY(launch_gemm_f64_store(dq + r0 * dp, dp, dc, dp, qn + r0, cn, (int)rows, (int)n,
-                                    (int)dp, metric, 1, sc, n, s));
-    }
-    if (!p.global_sort) {
-      RowSelArgs ra{};
-      ra.scores = sc;
-      ra.lds = n;
-      ra.rows = (int)rows;
-      ra.N = (int)n;
-      ra.k = (int)k;
-      ra.P = p.P;
-      ra.metric = metric;
-      ra.is_f64 = 1;
-      ra.index_base = 0;
-      ra.out_idx = oi + r0 * k;
-      ra.out_score = os + r0 * k;
-      HIP_TRY(launch_rowselect(ra, s));
-    } else {
-      HIP_TRY(launch_rowsort_global(sc, n, (int)rows, (int)n, 1, metric, w + p.off_keys, p.P2,
-                                    (int)k, 0u, oi + r0 * k, os + r0 * k, s));
-    }
-  }
+  if ((rc = topk_f64_device_impl(dq, dp, m, dc, dp, n, d, k, metric, 0u, oi, os, b + off_w, s))) return rc;
   {
     Timed t("d2h", s);
     HIP_TRY(hipMemcpyAsync(out_idx, oi, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
@@ -1692,6 +1835,30 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
   }
   HIP_TRY(hipStreamSynchronize(s));
   return PMM_OK;
+}
+
+int pmm_topk_f64_device(const double *q, int64_t ldq, int64_t m, const double *c, int64_t ldc, int64_t n,
+                        int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *out_idx,
+                        double *out_score, void *stream) {
+  int rc = validate_sizes(m, n, d, k, true);
+  if (rc) return rc;
+  if ((rc = check_metric(metric))) return rc;
+  if (m == 0 || k == 0) return PMM_OK;
+  if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
+  const int64_t dp = cdiv(d, 16) * 16;
+  if (d == 0 || ldq < dp || ldc < dp || ((uintptr_t)q & 15) || ((uintptr_t)c & 15))
+    return fail(PMM_ERR_ARG,
+                "device f64 inputs need row strides >= roundup(d, 16) (zero-padded) and 16-byte-aligned "
+                "bases (d=%lld ldq=%lld ldc=%lld)",
+                (long long)d, (long long)ldq, (long long)ldc);
+  int dev;
+  if ((rc = ensure_device(&dev))) return rc;
+  hipStream_t s = (hipStream_t)stream;
+  void *w;
+  if ((rc = arena(dev, s, f64_workspace_bytes(m, n, k, metric), &w))) return rc;
+  rc = topk_f64_device_impl(q, ldq, m, c, ldc, n, d, k, metric, index_base, out_idx, out_score, (char *)w, s);
+  if (rc) return rc;
+  return arena_record(dev, s);
 }
 
 int pmm_matmul_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d, float *out) {

@@ -178,6 +178,39 @@ hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, 
                                  int metric, int store_metric, double *out, int64_t ldo,
                                  hipStream_t s);
 hipError_t launch_rowselect(const RowSelArgs &a, hipStream_t s);
+// ---- fused f64 top-k (pmm_f64.hip) ----
+struct Ent;
+struct F64TopkArgs {
+  const double *q;           // this launch's rows (row stride ldq)
+  const double *c;           // the whole corpus (row stride ldc)
+  const double *qn, *cn;     // cosine: norms, euclidean: squared norms (qn: this launch's rows)
+  int64_t ldq, ldc;
+  int M, D;                  // rows; padded K (multiple of 16)
+  int col0, ncol;            // corpus columns [col0, col0 + ncol) of this chunk
+  int metric;
+  const unsigned long long *tkey;  // [M] row threshold: the k-th entry (key, index); (0, ~0) = accept all
+  const uint32_t *tidx;
+  unsigned *cnt;             // [M] buffer counts
+  Ent *cand;                 // [M][cap] candidate buffers
+  int cap;
+};
+struct F64SelArgs {
+  Ent *cand;
+  unsigned *cnt;
+  int cap, M, k, P;          // P: LDS entries per wave, a power of two >= cap
+  int mode;                  // 0: keep the best k + raise the thresholds; 1: write the final lists
+  unsigned long long *tkey;
+  uint32_t *tidx;
+  int metric;
+  uint32_t index_base;
+  uint32_t *out_idx;
+  double *out_score;
+  unsigned *overflow;        // set when a row's count exceeded cap (entries were dropped)
+};
+hipError_t launch_gemm_f64_topk(const F64TopkArgs &a, hipStream_t s);
+hipError_t launch_f64_select(const F64SelArgs &a, hipStream_t s);
+hipError_t launch_f64_reset(unsigned long long *tkey, uint32_t *tidx, unsigned *cnt, int m, unsigned *overflow,
+                            hipStream_t s);
 // full-row sort fallback for very large k
 hipError_t launch_rowsort_global(const void *scores, int64_t lds, int rows, int N, int is_f64,
                                  int metric, void *keys_ws, int P2, int k, uint32_t index_base,

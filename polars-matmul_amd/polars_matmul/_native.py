@@ -52,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "pmm_topk_f32",
     "pmm_topk_f32_ex",
     "pmm_topk_f64",
+    "pmm_topk_f64_device",
     "pmm_matmul_f32",
     "pmm_matmul_f64",
     "pmm_host_alloc",
@@ -128,6 +129,7 @@ _SIGS = {
     "pmm_topk_f32": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_topk_f32_ex": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _i32, _vp, _vp], _i32),
     "pmm_topk_f64": ([_vp, _i64, _vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
+    "pmm_topk_f64_device": ([_vp, _i64, _i64, _vp, _i64, _i64, _i64, _i64, _i32, _u32, _vp, _vp, _vp], _i32),
     "pmm_matmul_f32": ([_vp, _i64, _vp, _i64, _i64, _vp], _i32),
     "pmm_matmul_f64": ([_vp, _i64, _vp, _i64, _i64, _vp], _i32),
     "pmm_host_alloc": ([_sz, ctypes.POINTER(ctypes.c_void_p)], _i32),
@@ -398,6 +400,14 @@ def topk_device(q_ptr: int, ldq: int, m: int, c_ptr: int, ldc: int, n: int, d: i
     check(_lib.pmm_topk_f32_device(q_ptr, ldq, m, c_ptr, ldc, n, d, k, metric, compute,
                                    index_base, out_idx_ptr, out_score_ptr, workspace or None,
                                    workspace_bytes, stream or None))
+
+
+def topk_f64_device(q_ptr: int, ldq: int, m: int, c_ptr: int, ldc: int, n: int, d: int, k: int,
+                    metric: int, out_idx_ptr: int, out_score_ptr: int, *, index_base: int = 0,
+                    stream: int = 0) -> None:
+    """Device-resident f64 top-k (pmm_topk_f64_device; row strides >= roundup(d, 16))."""
+    check(_lib.pmm_topk_f64_device(q_ptr, ldq, m, c_ptr, ldc, n, d, k, metric, index_base, out_idx_ptr,
+                                   out_score_ptr, stream or None))
 
 
 def topk_bf16_device(q_ptr: int, ldq: int, m: int, c_ptr: int, ldc: int, n: int, d: int, k: int,

@@ -174,6 +174,90 @@ def test_f64_fixture_vs_oracle(pmm, metric):
     assert exact_match_rate(idx, oi) == 1.0
 
 
+# ---- the fused f64 path (pmm_f64.hip): chunked scan
+# with a running per-row k-th, against the oracle (src/metrics.rs:258-311 +
+# src/topk.rs:6-39 restated) and the materialised path (PMM_F64_FUSED=0) ----
+@pytest.mark.parametrize("m,n,d,k", [(48, 1000, 256, 50), (33, 30011, 37, 10), (7, 9000, 100, 1),
+                                     (64, 20000, 64, 100), (5, 3000, 16, 1000), (130, 700, 200, 700)])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_f64_fused_vs_oracle_and_materialised(pmm, m, n, d, k, metric, monkeypatch):
+    rs = np.random.RandomState(m * 7 + n + d + k)
+    q = rs.randn(m, d)
+    c = rs.randn(n, d)
+    c[n - 30:] = c[:30]  # exact ties across chunk boundaries
+    c[n // 2] = 0.0      # a zero-norm corpus row
+    q[0] = c[5]          # a query equal to a corpus row
+    idx, sc = gpu_topk(q, c, k, metric)
+    assert sc.dtype == np.float64 and idx.shape == (m, min(k, n))
+    oi, osc = oracle.topk(q, c, k, METRICS[metric])
+    assert exact_match_rate(idx, oi) == 1.0, f"f64 fused vs oracle {metric}"
+    np.testing.assert_allclose(sc, osc, rtol=1e-12, atol=1e-12)
+    monkeypatch.setenv("PMM_F64_FUSED", "0")
+    mi, ms = gpu_topk(q, c, k, metric)
+    assert np.array_equal(mi, idx)
+    np.testing.assert_allclose(ms, sc, rtol=1e-12, atol=1e-12)
+
+
+def test_f64_fused_scores_bitwise_vs_oracle(pmm):
+    # v_mfma_f64_16x16x4_f64 fed K in natural order (lane kq holds k0 + 4s + kq
+    # at step s): if the instruction accumulates its four products as a
+    # k-ordered fma chain, every score equals the oracle's bit for bit
+    rs = np.random.RandomState(77)
+    q, c = rs.randn(40, 256), rs.randn(5000, 256)
+    for metric in ("dot", "cosine", "euclidean"):
+        idx, sc = gpu_topk(q, c, 20, metric)
+        oi, osc = oracle.topk(q, c, 20, METRICS[metric])
+        assert np.array_equal(idx, oi)
+        assert np.array_equal(sc.view(np.uint64), osc.view(np.uint64)), metric
+
+
+def test_f64_fused_overflow_falls_back(pmm):
+    # adversarial order: every corpus row beats every earlier one, so each
+    # chunk's survivors overflow the buffers; the call must still be exact
+    # (materialised fallback)
+    n, d = 20000, 16
+    q = np.ones((4, d))
+    c = np.repeat(np.arange(n, dtype=np.float64)[:, None], d, axis=1) / n
+    idx, sc = gpu_topk(q, c, 10, "dot")
+    assert idx.tolist() == [list(range(n - 1, n - 11, -1))] * 4
+    oi, osc = oracle.topk(q, c, 10, METRICS["dot"])
+    assert np.array_equal(idx, oi) and np.array_equal(sc, osc)
+
+
+def test_f64_nan_rows_and_k_equals_n(pmm):
+    rs = np.random.RandomState(5)
+    q, c = rs.randn(9, 24), rs.randn(1500, 24)
+    c[[3, 700, 1499]] = np.nan
+    for metric in ("cosine", "dot", "euclidean"):
+        for k in (10, 1500):
+            idx, sc = gpu_topk(q, c, k, metric)
+            oi, osc = oracle.topk(q, c, k, METRICS[metric])
+            assert exact_match_rate(idx, oi) == 1.0, (metric, k)
+            np.testing.assert_allclose(sc, osc, rtol=1e-12, atol=1e-12, equal_nan=True)
+
+
+def test_f64_device_api_equals_host(pmm):
+    import torch
+
+    n = _native()
+    rs = np.random.RandomState(8)
+    q, c = rs.randn(100, 70), rs.randn(8000, 70)
+    want = n.topk_host(q, c, 25, METRICS["cosine"])
+    dev = torch.device("cuda", 0)
+    ld = 80  # >= roundup(70, 16), zero-padded
+    qd = torch.zeros((100, ld), dtype=torch.float64, device=dev)
+    cd = torch.zeros((8000, ld), dtype=torch.float64, device=dev)
+    qd[:, :70] = torch.from_numpy(q).to(dev)
+    cd[:, :70] = torch.from_numpy(c).to(dev)
+    oi = torch.empty((100, 25), dtype=torch.int32, device=dev)
+    os_ = torch.empty((100, 25), dtype=torch.float64, device=dev)
+    n.topk_f64_device(qd.data_ptr(), ld, 100, cd.data_ptr(), ld, 8000, 70, 25, METRICS["cosine"], oi.data_ptr(),
+                      os_.data_ptr(), index_base=1000, stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(oi.cpu().numpy().view(np.uint32) - 1000, want[0])
+    assert np.array_equal(os_.cpu().numpy(), want[1])
+
+
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
 def test_edge_fixture_exact(pmm, metric):
     # zero-norm rows, exact duplicate corpus rows (ties), d=37 (padded to 64)
