@@ -28,65 +28,139 @@ __device__ __forceinline__ double f64_unkey(u64 k, int metric) {
 }
 
 // ---------------------------------------------------------------------------
-// GEMM + epilogue + threshold append.  64 x 64 tile per 4-wave workgroup, each
-// wave 32 x 32 (2 x 2 MFMA tiles).  K step s of a 16-K chunk: lane (i = lane &
-// 15, kq = lane >> 4) feeds A[row i][k0 + 4 s + kq] and B[col i][k0 + 4 s + kq],
-// so the four MFMAs of a chunk see k0 .. k0 + 15 in natural order.  Operands
-// load straight from global memory (L2), the next chunk's while this one's
-// MFMAs run.  C/D layout: col = lane & 15, row = (lane >> 4) + 4 * reg.
+// The f64 GEMM tile (store mode and the fused top-k share it, so both paths
+// compute every dot product identically).  64 x 64 tile per 4-wave
+// workgroup, each wave 32 x 32 = 2 x 2 v_mfma_f64_16x16x4_f64 tiles.  K runs
+// in chunks of 16 through a double-buffered LDS image stored k-major
+// (As[k][row]), so at K step s of a chunk lane (i = lane & 15, kq = lane >> 4)
+// reads A[row i][k0 + 4 s + kq] and B[col i][k0 + 4 s + kq] with one
+// ds_read_b64 each: the four MFMAs of a chunk see k0 .. k0 + 15 in natural
+// order.  Rows of 16 + 64 doubles: the kq = 0 and kq = 1 half-waves of a read
+// land on disjoint banks.  Global loads: each thread one 32-byte run (row t/4,
+// k 4(t%4) .. +3) of A and of B per chunk, the next chunk's in flight while
+// this chunk's MFMAs run.  C/D layout: col = lane & 15, row = (lane >> 4) + 4 reg.
 // ---------------------------------------------------------------------------
-template <int METRIC>
-__global__ __launch_bounds__(256) void gemm_f64_topk_kernel(F64TopkArgs a) {
-  constexpr bool XF = METRIC != kMetricDot;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+constexpr int kF64LdsRow = 80;                              // doubles per LDS row (64 + pad)
+constexpr int kF64LdsBuf = 16 * kF64LdsRow;                 // one operand's chunk
+
+__device__ __forceinline__ void f64_tile(const double *__restrict__ q, int64_t ldq, int mrows,
+                                         const double *__restrict__ c, int64_t ldc, int ncols, int D,
+                                         f64x4 (&acc)[2][2], double *lds) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int i = lane & 15, kq = lane >> 4;
-  const int row0 = blockIdx.y * 64 + (wid >> 1) * 32;
-  const int lc0 = blockIdx.x * 64 + (wid & 1) * 32;  // column within the chunk
-  const double *ap[2], *bp[2];
-#pragma unroll
-  for (int t = 0; t < 2; t++) {
-    ap[t] = a.q + (int64_t)min(row0 + 16 * t + i, a.M - 1) * a.ldq + kq;
-    bp[t] = a.c + (int64_t)(a.col0 + min(lc0 + 16 * t + i, a.ncol - 1)) * a.ldc + kq;
-  }
-  f64x4 acc[2][2];
+  const int wr = (wid >> 1) * 32, wc = (wid & 1) * 32;
+  // this thread's staging run: row / column lr, k 4 lk .. 4 lk + 3 of a chunk
+  const int lr = tid >> 2, lk = (tid & 3) * 4;
+  const double *ga = q + (int64_t)min(lr, mrows - 1) * ldq + lk;
+  const double *gb = c + (int64_t)min(lr, ncols - 1) * ldc + lk;
+  double *As = lds, *Bs = lds + 2 * kF64LdsBuf;
 #pragma unroll
   for (int ti = 0; ti < 2; ti++)
 #pragma unroll
     for (int tj = 0; tj < 2; tj++) acc[ti][tj] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  double av[2][4], bv[2][4];
-#pragma unroll
-  for (int t = 0; t < 2; t++)
+  f64x2 ra0 = *(const f64x2 *)ga, ra1 = *(const f64x2 *)(ga + 2);
+  f64x2 rb0 = *(const f64x2 *)gb, rb1 = *(const f64x2 *)(gb + 2);
+  auto put = [&](int buf) __attribute__((always_inline)) {
+    double *a = As + buf * kF64LdsBuf + lk * kF64LdsRow + lr;
+    double *b = Bs + buf * kF64LdsBuf + lk * kF64LdsRow + lr;
+    a[0] = ra0[0];
+    a[kF64LdsRow] = ra0[1];
+    a[2 * kF64LdsRow] = ra1[0];
+    a[3 * kF64LdsRow] = ra1[1];
+    b[0] = rb0[0];
+    b[kF64LdsRow] = rb0[1];
+    b[2 * kF64LdsRow] = rb1[0];
+    b[3 * kF64LdsRow] = rb1[1];
+  };
+  put(0);
+  __syncthreads();
+  const int nch = D / 16;
+  for (int ch = 0; ch < nch; ch++) {
+    const int buf = ch & 1;
+    if (ch + 1 < nch) {
+      const int ko = (ch + 1) * 16;
+      ra0 = *(const f64x2 *)(ga + ko);
+      ra1 = *(const f64x2 *)(ga + ko + 2);
+      rb0 = *(const f64x2 *)(gb + ko);
+      rb1 = *(const f64x2 *)(gb + ko + 2);
+    }
+    const double *a = As + buf * kF64LdsBuf + kq * kF64LdsRow + wr + i;
+    const double *b = Bs + buf * kF64LdsBuf + kq * kF64LdsRow + wc + i;
 #pragma unroll
     for (int s = 0; s < 4; s++) {
-      av[t][s] = ap[t][4 * s];
-      bv[t][s] = bp[t][4 * s];
+      const double a0 = a[4 * s * kF64LdsRow], a1 = a[4 * s * kF64LdsRow + 16];
+      const double b0 = b[4 * s * kF64LdsRow], b1 = b[4 * s * kF64LdsRow + 16];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
     }
-  for (int k0 = 0; k0 < a.D; k0 += 16) {
-    double an[2][4], bn[2][4];
-    const int kn = k0 + 16 < a.D ? k0 + 16 : k0;  // (the last chunk re-reads itself)
-#pragma unroll
-    for (int t = 0; t < 2; t++)
-#pragma unroll
-      for (int s = 0; s < 4; s++) {
-        an[t][s] = ap[t][kn + 4 * s];
-        bn[t][s] = bp[t][kn + 4 * s];
-      }
-#pragma unroll
-    for (int s = 0; s < 4; s++)
-#pragma unroll
-      for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-        for (int tj = 0; tj < 2; tj++)
-          acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti][s], bv[tj][s], acc[ti][tj], 0, 0, 0);
-#pragma unroll
-    for (int t = 0; t < 2; t++)
-#pragma unroll
-      for (int s = 0; s < 4; s++) {
-        av[t][s] = an[t][s];
-        bv[t][s] = bn[t][s];
-      }
+    if (ch + 1 < nch) put(buf ^ 1);
+    __syncthreads();
   }
-  // epilogue: exact score, key, compare with the row's k-th, append
+}
+
+// Store mode (`.pmm.matmul` f64, src/metrics.rs:40-157; and the materialised
+// top-k path's transformed scores, :258-311).
+template <int METRIC, int XF>
+__global__ __launch_bounds__(256) void gemm_f64_store_kernel(const double *__restrict__ q, int64_t ldq,
+                                                             const double *__restrict__ c, int64_t ldc,
+                                                             const double *__restrict__ qn,
+                                                             const double *__restrict__ cn, int M, int N, int D,
+                                                             double *__restrict__ out, int64_t ldo) {
+  __shared__ double lds[2 * 2 * kF64LdsBuf];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  f64x4 acc[2][2];
+  f64_tile(q + (int64_t)r0 * ldq, ldq, M - r0, c + (int64_t)c0 * ldc, ldc, N - c0, D, acc, lds);
+  const int row0 = r0 + (wid >> 1) * 32, col0 = c0 + (wid & 1) * 32;
+#pragma unroll
+  for (int ti = 0; ti < 2; ti++)
+#pragma unroll
+    for (int tj = 0; tj < 2; tj++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int grow = row0 + 16 * ti + kq + 4 * r;
+        const int gcol = col0 + 16 * tj + i;
+        if (grow < M && gcol < N) {
+          const double v = acc[ti][tj][r];
+          out[(int64_t)grow * ldo + gcol] = XF ? exact_score_f64<METRIC>(v, qn[grow], cn[gcol]) : v;
+        }
+      }
+}
+
+hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, int64_t ldc,
+                                 const double *qn, const double *cn, int M, int N, int D,
+                                 int metric, int store_metric, double *out, int64_t ldo,
+                                 hipStream_t s) {
+  if (M <= 0 || N <= 0) return hipSuccess;
+  const dim3 grid((N + 63) / 64, (M + 63) / 64), blk(256);
+  if (!store_metric || metric == kMetricDot)
+    gemm_f64_store_kernel<kMetricDot, 0><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
+  else if (metric == kMetricCosine)
+    gemm_f64_store_kernel<kMetricCosine, 1><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
+  else
+    gemm_f64_store_kernel<kMetricEuclidean, 1><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Fused top-k pass over one column chunk: the tile above, then per element
+// the exact score (reference order), its key, and an append to the row's
+// buffer when it beats the row's threshold.
+// ---------------------------------------------------------------------------
+template <int METRIC>
+__global__ __launch_bounds__(256) void gemm_f64_topk_kernel(F64TopkArgs a) {
+  constexpr bool XF = METRIC != kMetricDot;
+  __shared__ double lds[2 * 2 * kF64LdsBuf];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i = lane & 15, kq = lane >> 4;
+  const int r0 = blockIdx.y * 64, lc0w = blockIdx.x * 64;  // lc: column within the chunk
+  f64x4 acc[2][2];
+  f64_tile(a.q + (int64_t)r0 * a.ldq, a.ldq, a.M - r0, a.c + (int64_t)(a.col0 + lc0w) * a.ldc, a.ldc,
+           a.ncol - lc0w, a.D, acc, lds);
+  const int row0 = r0 + (wid >> 1) * 32, lc0 = lc0w + (wid & 1) * 32;
 #pragma unroll
   for (int ti = 0; ti < 2; ti++)
 #pragma unroll

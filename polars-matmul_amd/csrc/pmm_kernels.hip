@@ -1175,83 +1175,7 @@ hipError_t launch_merge(const MergeArgs &a0, int loader, hipStream_t s) {
   return hipGetLastError();
 }
 
-// ===========================================================================
-// f64 GEMM (store mode) on v_mfma_f64_16x16x4_f64, for the f64 path
-// (src/metrics.rs:40-157, 258-311).  64x64 tile per 4-wave workgroup, each
-// wave 32x32 = 2x2 MFMA tiles; fragments load straight from global (L2).
-// C/D layout of the f64 MFMA: col = lane&15, row = (lane>>4) + 4*reg.
-// ===========================================================================
-template <int METRIC, int XF>
-__global__ __launch_bounds__(256) void gemm_f64_kernel(const double *__restrict__ q, int64_t ldq,
-                                                       const double *__restrict__ c, int64_t ldc,
-                                                       const double *__restrict__ qn,
-                                                       const double *__restrict__ cn, int M, int N,
-                                                       int D, double *__restrict__ out,
-                                                       int64_t ldo) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int i = lane & 15, kq = lane >> 4;
-  const int row0 = blockIdx.y * 64 + (wid >> 1) * 32;
-  const int col0 = blockIdx.x * 64 + (wid & 1) * 32;
-  const double *ap[2], *bp[2];
-#pragma unroll
-  for (int t = 0; t < 2; t++) {
-    ap[t] = q + (int64_t)min(row0 + 16 * t + i, M - 1) * ldq + 4 * kq;
-    bp[t] = c + (int64_t)min(col0 + 16 * t + i, N - 1) * ldc + 4 * kq;
-  }
-  f64x4 acc[2][2];
-#pragma unroll
-  for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-    for (int tj = 0; tj < 2; tj++) acc[ti][tj] = (f64x4){};
-  for (int k0 = 0; k0 < D; k0 += 16) {
-    f64x2 av[2][2], bv[2][2];
-#pragma unroll
-    for (int t = 0; t < 2; t++) {
-      av[t][0] = *(const f64x2 *)(ap[t] + k0);
-      av[t][1] = *(const f64x2 *)(ap[t] + k0 + 2);
-      bv[t][0] = *(const f64x2 *)(bp[t] + k0);
-      bv[t][1] = *(const f64x2 *)(bp[t] + k0 + 2);
-    }
-#pragma unroll
-    for (int st = 0; st < 4; st++)
-#pragma unroll
-      for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-        for (int tj = 0; tj < 2; tj++)
-          acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti][st >> 1][st & 1],
-                                                              bv[tj][st >> 1][st & 1],
-                                                              acc[ti][tj], 0, 0, 0);
-  }
-#pragma unroll
-  for (int ti = 0; ti < 2; ti++)
-#pragma unroll
-    for (int tj = 0; tj < 2; tj++)
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int grow = row0 + 16 * ti + kq + 4 * r;
-        const int gcol = col0 + 16 * tj + i;
-        if (grow < M && gcol < N) {
-          const double v = acc[ti][tj][r];
-          out[(int64_t)grow * ldo + gcol] =
-              XF ? exact_score_f64<METRIC>(v, qn[grow], cn[gcol]) : v;
-        }
-      }
-}
-
-hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, int64_t ldc,
-                                 const double *qn, const double *cn, int M, int N, int D,
-                                 int metric, int store_metric, double *out, int64_t ldo,
-                                 hipStream_t s) {
-  if (M <= 0 || N <= 0) return hipSuccess;
-  const dim3 grid((N + 63) / 64, (M + 63) / 64), blk(256);
-  if (!store_metric || metric == kMetricDot)
-    gemm_f64_kernel<kMetricDot, 0><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
-  else if (metric == kMetricCosine)
-    gemm_f64_kernel<kMetricCosine, 1><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
-  else
-    gemm_f64_kernel<kMetricEuclidean, 1><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
-  return hipGetLastError();
-}
+// (the f64 GEMM, store mode and fused top-k: pmm_f64.hip)
 
 // ===========================================================================
 // Row-select over materialised (metric-transformed) scores: one wave per row
