@@ -1405,7 +1405,7 @@ int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double 
     uint32_t *tidx = (uint32_t *)(w + p.off_tidx);
     unsigned *cnt = (unsigned *)(w + p.off_cnt);
     Ent *cand = (Ent *)(w + p.off_cand);
-    HIP_TRY(launch_f64_reset(tkey, tidx, cnt, rows, flag + 1, s));
+    HIP_TRY(launch_f64_reset(tkey, tidx, cnt, rows, (unsigned)s0, s));
     F64TopkArgs a{};
     a.q = dq + r0 * ldq;
     a.c = dc;
@@ -1440,6 +1440,7 @@ int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double 
       const int64_t cc = std::min<int64_t>(chunk, n - seen);
       a.col0 = (int)seen;
       a.ncol = (int)cc;
+      a.accept_all = seen == 0;  // (s0 <= cap / 2)
       {
         Timed t("gemm_f64_topk", s);
         HIP_TRY(launch_gemm_f64_topk(a, s));

@@ -178,7 +178,15 @@ __global__ __launch_bounds__(256) void gemm_f64_topk_kernel(F64TopkArgs a) {
         const double v = acc[ti][tj][r];
         const double sc = XF ? exact_score_f64<METRIC>(v, qv, a.cn[gcol]) : v;
         const u64 key = f64_key(sc, METRIC);
-        if (key > tk || (key == tk && gcol < tx)) {
+        if (a.accept_all) {
+          // the first chunk (ncol <= cap): every element, at its own column's
+          // slot (the counts were set to ncol by the reset; no atomics)
+          Ent e;
+          e.key = key;
+          e.idx = gcol;
+          e.pad = 0u;
+          a.cand[(int64_t)row * a.cap + lc] = e;
+        } else if (key > tk || (key == tk && gcol < tx)) {
           const unsigned pos = atomicAdd(a.cnt + row, 1u);
           if (pos < (unsigned)a.cap) {
             Ent e;
@@ -260,20 +268,19 @@ __global__ __launch_bounds__(256) void f64_select_kernel(F64SelArgs a) {
   }
 }
 
-// thresholds to accept-all, counts to 0
+// thresholds to accept-all, counts to cnt0 (the first chunk's width)
 __global__ __launch_bounds__(256) void f64_reset_kernel(u64 *tkey, uint32_t *tidx, unsigned *cnt, int m,
-                                                        unsigned *overflow) {
+                                                        unsigned cnt0) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r == 0) *overflow = 0u;
   if (r < m) {
     tkey[r] = 0ull;
     tidx[r] = 0xFFFFFFFFu;
-    cnt[r] = 0u;
+    cnt[r] = cnt0;
   }
 }
 
-hipError_t launch_f64_reset(u64 *tkey, uint32_t *tidx, unsigned *cnt, int m, unsigned *overflow, hipStream_t s) {
-  f64_reset_kernel<<<(m + 255) / 256, 256, 0, s>>>(tkey, tidx, cnt, m, overflow);
+hipError_t launch_f64_reset(u64 *tkey, uint32_t *tidx, unsigned *cnt, int m, unsigned cnt0, hipStream_t s) {
+  f64_reset_kernel<<<(m + 255) / 256, 256, 0, s>>>(tkey, tidx, cnt, m, cnt0);
   return hipGetLastError();
 }
 

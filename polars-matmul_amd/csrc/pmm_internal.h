@@ -193,6 +193,7 @@ struct F64TopkArgs {
   unsigned *cnt;             // [M] buffer counts
   Ent *cand;                 // [M][cap] candidate buffers
   int cap;
+  int accept_all;            // first chunk (ncol <= cap): every element at slot = its chunk column
 };
 struct F64SelArgs {
   Ent *cand;
@@ -209,7 +210,7 @@ struct F64SelArgs {
 };
 hipError_t launch_gemm_f64_topk(const F64TopkArgs &a, hipStream_t s);
 hipError_t launch_f64_select(const F64SelArgs &a, hipStream_t s);
-hipError_t launch_f64_reset(unsigned long long *tkey, uint32_t *tidx, unsigned *cnt, int m, unsigned *overflow,
+hipError_t launch_f64_reset(unsigned long long *tkey, uint32_t *tidx, unsigned *cnt, int m, unsigned cnt0,
                             hipStream_t s);
 // full-row sort fallback for very large k
 hipError_t launch_rowsort_global(const void *scores, int64_t lds, int rows, int N, int is_f64,
