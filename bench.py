@@ -602,7 +602,7 @@ def kernel_stats(bf16):
         out[key] = (ms / n if n else None, n)
     if bf16:
         # which bf16 kernel ran (the library's timer names carry it)
-        out["bf16_kernel"] = next((v for v in ("r64", "dsx", "ws", "one-wave")
+        out["bf16_kernel"] = next((v for v in ("r64", "ws", "one-wave")
                                    if _native.timing_read("gemm_bf16_topk/" + v)[1]), "ws")
     return out
 
@@ -610,8 +610,6 @@ def kernel_stats(bf16):
 BF16_KERNEL_NAMES = {
     "r64": "gemm_bf16_r64_kernel (256 query rows held by one wave per SIMD: fused GEMM + metric + top-k; "
            "+ seed_bf16_ws_kernel in achieved)",
-    "dsx": "gemm_bf16_dsx_kernel (256 query rows, K split over wave pairs: fused GEMM + metric + "
-           "top-k; + seed_bf16_dsx_kernel in achieved)",
     "ws": "gemm_bf16_ws_kernel (wave-specialised fused GEMM + metric + top-k; "
           "+ seed_bf16_ws_kernel in achieved)",
     "one-wave": "gemm_bf16_kernel (one-wave fused GEMM + metric + top-k)",

@@ -148,15 +148,6 @@ hipError_t launch_gemm_bf16_ws(const GemmF32Args &a, int grid, hipStream_t s);
 // bf16 threshold seed (pmm_bf16_ws_kernel.h): S[row][0..ns) = the scores of
 // corpus rows 0..ns-1 exactly as the wave-specialised kernel computes them
 hipError_t launch_seed_bf16_ws(const GemmF32Args &a, float *S, int ns, hipStream_t s);
-// 256-query-row bf16 kernel (pmm_bf16_dsx_kernel.h): each wave pair holds 64
-// query rows x the two halves of D, 16-column corpus tiles, 8 waves in two
-// half-tile-staggered groups.  Padded D in {256, 512, 768}; capg <=
-// kBf16WsMaxCapg.
-constexpr int kBf16DsxBM = 256, kBf16DsxBN = 16;
-bool bf16_dsx_supported(int D);  // D = padded dimension
-size_t gemm_bf16_dsx_lds_bytes(int D);
-hipError_t launch_gemm_bf16_dsx(const GemmF32Args &a, int grid, hipStream_t s);
-hipError_t launch_seed_bf16_dsx(const GemmF32Args &a, float *S, int ns, hipStream_t s);
 // 256-query-row bf16 kernel held by one wave per SIMD (pmm_bf16_r64_kernel.h):
 // 64 rows x D per wave (AGPRs + VGPRs), 32-column corpus tiles, the epilogue
 // on the same wave between the MFMAs.  The wave-specialised kernel's
