@@ -914,21 +914,71 @@ def inproc_child(args) -> None:
     dc.close()
 
 
-def run_inproc_child(args, world):
+class EarlySpawner:
+    """A helper process forked BEFORE this process touches the GPU, which later
+    starts one program on request and returns its exit status and output.  A
+    process that has initialised the GPU must not exec another program; the
+    helper never initialises it, so the program it starts is clean."""
+
+    def __init__(self):
+        r1, w1 = os.pipe()
+        r2, w2 = os.pipe()
+        pid = os.fork()
+        if pid == 0:  # the helper: no GPU, no torch
+            os.close(w1)
+            os.close(r2)
+            code = 0
+            try:
+                with os.fdopen(r1, "rb") as f:
+                    req = f.read()
+                if req:
+                    job = json.loads(req)
+                    try:
+                        r = subprocess.run(job["cmd"], env=job["env"], capture_output=True, text=True,
+                                           timeout=job["timeout"])
+                        res = {"rc": r.returncode, "stdout": r.stdout, "stderr": r.stderr}
+                    except subprocess.TimeoutExpired:
+                        res = {"rc": None, "stdout": "", "stderr": f"timed out after {job['timeout']} s"}
+                    with os.fdopen(w2, "wb") as f:
+                        f.write(json.dumps(res).encode())
+            except Exception:
+                code = 1
+            os._exit(code)
+        os.close(r1)
+        os.close(w2)
+        self.pid, self.w, self.r = pid, w1, r2
+
+    def run(self, cmd, env, timeout):
+        with os.fdopen(self.w, "wb") as f:
+            f.write(json.dumps({"cmd": cmd, "env": env, "timeout": timeout}).encode())
+        self.w = None
+        with os.fdopen(self.r, "rb") as f:
+            out = f.read()
+        self.r = None
+        os.waitpid(self.pid, 0)
+        return json.loads(out) if out else {"rc": None, "stdout": "", "stderr": "helper failed"}
+
+    def close(self):
+        if self.w is not None:  # never used: let the helper exit
+            os.close(self.w)
+            os.close(self.r)
+            os.waitpid(self.pid, 0)
+            self.w = self.r = None
+
+
+def run_inproc_child(args, world, spawner):
     """Start the in-process transport measurement as a fresh child process
-    (no torch.distributed env) and return its JSON record."""
+    (through the early helper; no torch.distributed env) and return its JSON
+    record."""
     env = {kk: v for kk, v in os.environ.items()
            if kk not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
                          "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID")}
     cmd = [sys.executable, os.path.abspath(__file__), "--inproc-child", str(world), "--config", args.config,
            "--steps", str(args.steps), "--warmup", str(args.warmup)]
-    try:
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=args.inproc_timeout)
-    except subprocess.TimeoutExpired:
-        return {"error": f"in-process child timed out after {args.inproc_timeout} s"}
-    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
-    if r.returncode != 0 or not lines:
-        return {"error": f"in-process child rc={r.returncode}", "stderr_tail": r.stderr[-800:]}
+    r = spawner.run(cmd, env, args.inproc_timeout)
+    lines = [x for x in r["stdout"].splitlines() if x.startswith("{")]
+    if r["rc"] != 0 or not lines:
+        return {"error": f"in-process child rc={r['rc']}", "stderr_tail": r["stderr"][-800:]}
     return json.loads(lines[-1])
 
 
@@ -1029,6 +1079,9 @@ def main():
         return
     if args.cpu_threads <= 0:
         args.cpu_threads = available_parallelism()
+    # rank 0 of an N > 1 run starts the in-process transport's measurement
+    # after the RCCL one: fork its helper now, before anything touches the GPU
+    spawner = EarlySpawner() if (world > 1 and rank == 0 and args.inproc) else None
 
     import torch
 
@@ -1118,7 +1171,7 @@ def main():
         # drives all N GPUs through the drop-in boundary
         del q, c
         torch.cuda.empty_cache()
-        inproc = run_inproc_child(args, world)
+        inproc = run_inproc_child(args, world, spawner)
         log(f"inproc: {inproc}")
 
     line = {
@@ -1148,6 +1201,8 @@ def main():
         "check": fields["check"],
     }
     print(json.dumps(line), flush=True)
+    if spawner:
+        spawner.close()
     if dist:
         dist.destroy_process_group()
 

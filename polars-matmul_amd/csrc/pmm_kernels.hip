@@ -943,8 +943,105 @@ struct PrologueArgs {
   uint4 *z0, *z1;              // zeroed ranges (16-byte words)
   int64_t z0n, z1n;
   unsigned sblocks, qblocks, cblocks, zblocks;
+  int mfma_seed;               // seed blocks of 32 rows on the f32 MFMA (seed_mfma_block)
 };
+
+// MFMA seed block: query rows 32 b .. 32 b + 31 against all ns sample columns
+// on v_mfma_f32_32x32x2_f32 -- the fused kernel's instruction with its
+// operand values in its order: substep t pairs k = 2t (lane half 0) with
+// 2t + 1 (half 1), from the first substep onto zeros, so every score is the
+// main pass's bit for bit.  Operands come straight from global memory as
+// 16-byte pieces (k = 8 j + 4 h .. + 3 on half h) and two v_permlane32_swap per
+// piece turn them into the natural-order pairs (the fused kernel's K order 1).
+// Wave w computes the 32 x 32 tiles of sample columns 32 (w + 4 i); the row
+// and column norms in ndarray order from the same rows (norms_rows), the
+// composite keys into LDS, then each wave selects 8 rows' k-th.  Against
+// seed_dots (4 rows per block, one sample column per thread as fmaf chains,
+// each thread streaming its own 1 KiB row: 19 us at c1, latency-bound) the
+// work is MFMA-paced: 128 MFMAs per tile at D = 256.
 template <int E, int METRIC>
+__device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned b, char *smem) {
+  constexpr bool XFORM = METRIC != kMetricDot;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int ns = a.ns, dp = a.dp, NSP = 64 * E;
+  u64 *keys = (u64 *)smem;                        // [32][NSP]
+  float *qn_s = (float *)(smem + 32 * NSP * 8);   // [32]
+  float *cn_s = qn_s + 32;                        // [NSP]
+  const int row0 = (int)b * 32;
+  if (XFORM) {
+    norms_rows<float, float>(a.q + (int64_t)row0 * a.ldq, min(32, a.m - row0), a.d, a.ldq, a.squared, qn_s,
+                             nullptr, tid);
+    for (int g = tid; g < ns * 8; g += 256) norms_rows<float, float>(a.c, ns, a.d, a.ldc, a.squared, cn_s, nullptr, g);
+  }
+  const __amdgpu_buffer_rsrc_t ra =
+      make_rsrc(a.q + (int64_t)row0 * a.ldq, (int64_t)min(32, a.m - row0) * a.ldq * 4);
+  auto kpair = [](f32x4 &x) __attribute__((always_inline)) {
+    auto r0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[0]), __float_as_uint(x[1]), false, false);
+    auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[2]), __float_as_uint(x[3]), false, false);
+    x[0] = __uint_as_float(r0[0]);
+    x[1] = __uint_as_float(r0[1]);
+    x[2] = __uint_as_float(r1[0]);
+    x[3] = __uint_as_float(r1[1]);
+  };
+  const uint32_t aoff = (uint32_t)(r32 * a.ldq * 4 + h * 16);
+  const int nj = dp / 8;
+  for (int ct = w; ct < ns / 32; ct += 4) {
+    const int col0 = ct * 32;
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.c + (int64_t)col0 * a.ldc, (int64_t)32 * a.ldc * 4);
+    const uint32_t boff = (uint32_t)(r32 * a.ldc * 4 + h * 16);
+    f32x16 acc = {};
+    constexpr int PD = 8;  // pieces in flight per operand
+    f32x4 ap[PD], bp[PD];
+#pragma unroll
+    for (int i = 0; i < PD; i++) {
+      const int j = min(i, nj - 1);
+      ap[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(aoff + j * 32), 0, 0));
+      bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (int)(boff + j * 32), 0, 0));
+    }
+    for (int j0 = 0; j0 < nj; j0 += PD) {
+#pragma unroll
+      for (int i = 0; i < PD; i++) {
+        f32x4 av = ap[i], bv = bp[i];
+        const int jn = min(j0 + i + PD, nj - 1);
+        ap[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(aoff + jn * 32), 0, 0));
+        bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (int)(boff + jn * 32), 0, 0));
+        kpair(av);
+        kpair(bv);
+#pragma unroll
+        for (int jj = 0; jj < 4; jj++) {
+          const int js = ((jj & 1) << 1) | (jj >> 1);  // swapped registers: {0, 2, 1, 3}
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[js], bv[js], acc, 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();  // (first tile: the norms in LDS; later: nothing, kept uniform)
+    const int col = col0 + r32;
+    const float cnv = XFORM ? cn_s[col] : 0.0f;
+#pragma unroll
+    for (int e = 0; e < 16; e++) {
+      const int r = acc_row(e, h);
+      u64 key = 0ull;
+      if (row0 + r < a.m) {
+        const float sc = exact_score<METRIC>(acc[e], XFORM ? qn_s[r] : 0.0f, cnv);
+        key = ((u64)okey32(METRIC == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~(uint32_t)col);
+      }
+      keys[r * NSP + col] = key;
+    }
+  }
+  for (int i = tid; i < 32 * NSP; i += 256)
+    if ((i % NSP) >= ns) keys[i] = 0ull;  // columns past the sample
+  __syncthreads();
+  for (int r = w * 8; r < w * 8 + 8; r++) {
+    if (row0 + r >= a.m) break;
+    u64 x[E];
+#pragma unroll
+    for (int e = 0; e < E; e++) x[e] = keys[r * NSP + lane + 64 * e];
+    const u64 th = wave_kth_u64<E>(x, a.k);
+    if (lane == 0) a.gthr[row0 + r] = th ? th - 1 : 0ull;
+  }
+}
+template <int E, int METRIC, int MFMA>
 __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   using namespace seedk;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -967,6 +1064,12 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
       if (i < a.z0n) a.z0[i] = make_uint4(0u, 0u, 0u, 0u);
       else a.z1[i - a.z0n] = make_uint4(0u, 0u, 0u, 0u);
     }
+    return;
+  }
+  if (MFMA) {
+    // (a template parameter, not a branch: the fmaf-chain seed's registers
+    // would otherwise set this path's occupancy too)
+    seed_mfma_block<E, METRIC>(a, b, smem);
     return;
   }
   constexpr bool XFORM = METRIC != kMetricDot;
@@ -1064,27 +1167,34 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   if (lane == 0) a.gthr[row] = th ? th - 1 : 0ull;
 }
 
-template <int METRIC>
-static hipError_t launch_prologue_t(const PrologueArgs &a, unsigned grid, hipStream_t s) {
+template <int METRIC, int MFMA>
+static hipError_t launch_prologue_t2(const PrologueArgs &a, unsigned grid, hipStream_t s) {
   using namespace seedk;
   const size_t lds_base = (size_t)RQ * a.dp * 4 + RQ * 4;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void *)prologue_kernel<4, METRIC>,
+    hipError_t e = hipFuncSetAttribute((const void *)prologue_kernel<4, METRIC, MFMA>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void *)prologue_kernel<8, METRIC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+      e = hipFuncSetAttribute((const void *)prologue_kernel<8, METRIC, MFMA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void *)prologue_kernel<16, METRIC>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+      e = hipFuncSetAttribute((const void *)prologue_kernel<16, METRIC, MFMA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  if (a.ns <= 256) prologue_kernel<4, METRIC><<<grid, 256, lds_base + RQ * 256 * 8, s>>>(a);
-  else if (a.ns <= 512) prologue_kernel<8, METRIC><<<grid, 256, lds_base + RQ * 512 * 8, s>>>(a);
-  else prologue_kernel<16, METRIC><<<grid, 256, lds_base + RQ * 1024 * 8, s>>>(a);
+  // (MFMA seed blocks: 32 rows' keys + norms in LDS)
+  auto lds = [&](int nsp) { return MFMA ? (size_t)32 * nsp * 8 + 4 * (32 + nsp) : lds_base + RQ * nsp * 8; };
+  if (a.ns <= 256) prologue_kernel<4, METRIC, MFMA><<<grid, 256, lds(256), s>>>(a);
+  else if (a.ns <= 512) prologue_kernel<8, METRIC, MFMA><<<grid, 256, lds(512), s>>>(a);
+  else if (!MFMA) prologue_kernel<16, METRIC, MFMA><<<grid, 256, lds(1024), s>>>(a);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
+}
+template <int METRIC>
+static hipError_t launch_prologue_t(const PrologueArgs &a, unsigned grid, hipStream_t s) {
+  return a.mfma_seed ? launch_prologue_t2<METRIC, 1>(a, grid, s) : launch_prologue_t2<METRIC, 0>(a, grid, s);
 }
 
 hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int64_t n,
@@ -1118,7 +1228,11 @@ hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const floa
   a.z1 = (uint4 *)z1;
   a.z0n = (int64_t)(z0_bytes / 16);
   a.z1n = (int64_t)(z1_bytes / 16);
-  a.sblocks = (unsigned)((m + seedk::RQ - 1) / seedk::RQ);
+  // MFMA seed blocks (seed_mfma_block) when the sample's keys fit LDS
+  // (PMM_SEED_MFMA=0, read per call: the fmaf-chain seed blocks)
+  const char *sme = getenv("PMM_SEED_MFMA");
+  a.mfma_seed = (ns % 32 == 0 && ns <= 512 && !(sme && atoi(sme) == 0)) ? 1 : 0;
+  a.sblocks = a.mfma_seed ? (unsigned)((m + 31) / 32) : (unsigned)((m + seedk::RQ - 1) / seedk::RQ);
   const bool xf = metric != kMetricDot;
   a.qblocks = xf ? (unsigned)((m * 8 + 255) / 256) : 0u;
   a.cblocks = (xf && corpus_norms) ? (unsigned)((n * 8 + 255) / 256) : 0u;

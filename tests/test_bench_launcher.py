@@ -41,3 +41,17 @@ def test_world_size_must_match_gpus():
     r = _run(["--gpus", "2", "--cpu-selftest"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2
     assert "WORLD_SIZE" in r.stderr
+
+
+def test_early_spawner_runs_a_program_and_returns_its_output():
+    # bench.py forks this helper before the GPU is touched; later the helper
+    # starts the in-process transport's child (a clean process) and hands back
+    # its status and output
+    import bench
+
+    sp = bench.EarlySpawner()
+    r = sp.run([sys.executable, "-c", "import sys; print('{\"ok\": 1}'); sys.exit(3)"], dict(os.environ), 60)
+    assert r["rc"] == 3 and r["stdout"].strip() == '{"ok": 1}'
+    sp.close()  # already used: no-op
+    unused = bench.EarlySpawner()
+    unused.close()  # the helper exits without running anything

@@ -922,12 +922,38 @@ def test_threshold_seeding_changes_nothing(pmm, k, d, monkeypatch):
         monkeypatch.setenv("PMM_SEED_GEMM", "1")
         got_g = gpu_topk(q, c, k, metric)
         monkeypatch.delenv("PMM_SEED_GEMM")
+        monkeypatch.setenv("PMM_SEED_MFMA", "0")  # the fmaf-chain seed blocks
+        got_f = gpu_topk(q, c, k, metric)
+        monkeypatch.delenv("PMM_SEED_MFMA")
         monkeypatch.delenv("PMM_SEED")
-        for g in (got, got_g):
+        for g in (got, got_g, got_f):
             assert np.array_equal(g[0], want[0]), metric
             assert np.array_equal(g[1], want[1]), metric
         check_topk(got[0], got[1], truth_scores(q, c, metric), metric != "euclidean",
                    label=f"seeded k={k} {metric}")
+
+
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+@pytest.mark.parametrize("seed_mfma", ["1", "0"])
+def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, seed_mfma, monkeypatch):
+    # Every row's true top-k lies inside the seed sample (the corpus's first
+    # ns = 256 rows hold 16 near-copies of each query).  The seed's threshold
+    # is (the sample's k-th composite) - 1, so if the seed scored the k-th
+    # element even one ulp above the main pass, the main pass would reject
+    # that element and the list would lose it: bit-exactness against the
+    # oracle here checks that the seed (MFMA blocks or fmaf chains) computes
+    # the main pass's scores bit for bit
+    rs = np.random.RandomState(17 + METRICS[metric])
+    m, N, d, k = 16, 4096, 256, 10
+    q = rs.randn(m, d).astype(np.float32)
+    c = (rs.randn(N, d) * 3.0).astype(np.float32)
+    c[:256] = q[np.arange(256) % m] + 0.05 * rs.randn(256, d).astype(np.float32)
+    monkeypatch.setenv("PMM_SEED", "1")
+    monkeypatch.setenv("PMM_SEED_MFMA", seed_mfma)
+    idx, sc = gpu_topk(q, c, k, metric)
+    assert int(idx.max()) < 256  # the top-k really is inside the sample
+    oi, osc = oracle.topk(q, c, k, METRICS[metric])
+    assert_bitexact(idx, sc, oi, osc, f"seed-sample top-k {metric} mfma={seed_mfma}")
 
 
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
