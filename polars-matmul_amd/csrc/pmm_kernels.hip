@@ -1002,6 +1002,7 @@ __device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned 
     for (int j0 = 0; j0 < nj; j0 += PD) {
 #pragma unroll
       for (int i = 0; i < PD; i++) {
+        if (j0 + i >= nj) break;  // (nj = dp / 8 is a multiple of 4, not of PD)
         f32x4 av = ap[i], bv = bp[i];
         const int jn = min(j0 + i + PD, nj - 1);
         ap[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(aoff + jn * 32), 0, 0));

@@ -935,7 +935,8 @@ def test_threshold_seeding_changes_nothing(pmm, k, d, monkeypatch):
 
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
 @pytest.mark.parametrize("seed_mfma", ["1", "0"])
-def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, seed_mfma, monkeypatch):
+@pytest.mark.parametrize("d", [256, 96, 37])
+def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, seed_mfma, d, monkeypatch):
     # Every row's true top-k lies inside the seed sample (the corpus's first
     # ns = 256 rows hold 16 near-copies of each query).  The seed's threshold
     # is (the sample's k-th composite) - 1, so if the seed scored the k-th
@@ -943,8 +944,8 @@ def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, see
     # that element and the list would lose it: bit-exactness against the
     # oracle here checks that the seed (MFMA blocks or fmaf chains) computes
     # the main pass's scores bit for bit
-    rs = np.random.RandomState(17 + METRICS[metric])
-    m, N, d, k = 16, 4096, 256, 10
+    rs = np.random.RandomState(17 + METRICS[metric] + d)
+    m, N, k = 16, 4096, 10
     q = rs.randn(m, d).astype(np.float32)
     c = (rs.randn(N, d) * 3.0).astype(np.float32)
     c[:256] = q[np.arange(256) % m] + 0.05 * rs.randn(256, d).astype(np.float32)
@@ -1091,7 +1092,9 @@ def test_set_devices_one_entry_runs_there(pmm, device_list):
     n.set_devices([0])
     assert n.get_devices() == [0]
     got = n.topk_host(q, c, 20, METRICS["cosine"])
-    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1])
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1].view(np.uint32), want[1].view(np.uint32))
+    oi, osc = oracle.topk(q, c, 20, METRICS["cosine"])
+    assert_bitexact(got[0], got[1], oi, osc, "one-entry device list")
     dc = n.DeviceCorpus(c)
     assert dc.shards == 1
     assert np.array_equal(dc.topk(q, 1500, METRICS["dot"])[0], n.topk_host(q, c, 1500, METRICS["dot"])[0])

@@ -10,7 +10,7 @@ if [ ! -s gpurun_out/r4b/probe16.txt ]; then
   done
   cd ../..
 fi
-timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "seed or r64 or set_devices or pinned" --timeout 400 --timeout-method thread > gpurun_out/r4c/gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x -k "seed or r64 or set_devices or pinned or oracle or fixture or kat or ref_" --timeout 400 --timeout-method thread > gpurun_out/r4c/gpu.log 2>&1
 rc=$?
 echo "gpu tests rc=$rc"; tail -3 gpurun_out/r4c/gpu.log
 [ $rc -eq 0 ] || exit $rc
