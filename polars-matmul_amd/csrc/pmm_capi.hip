@@ -243,8 +243,15 @@ struct Plan {
   int QB = 0, T = 0, tps = 0, S = 0, units = 0, grid = 0, capg = 0, P = 0, qb_full = 0;
   size_t off_counter = 0, off_gthr = 0, off_cnt = 0, off_cand = 0, off_qn = 0, off_cn = 0;
   size_t off_wq = 0;
+  // fire-and-forget bf16 kernel (variant -6): guess sample size and rank,
+  // region capacity; survivor counts, regions, the re-run row list
+  int ff_ns = 0, ff_j = 0, ffcap = 0;
+  size_t off_ffcnt = 0, off_ffreg = 0, off_fb = 0;
   size_t total = 0;
 };
+// set while a call re-runs the rows the fire-and-forget kernel could not
+// prove exact (they go to the wave-specialised kernel)
+thread_local bool t_no_ff = false;
 
 void plan_units(int64_t m, int64_t n, int bm, int bn, int cus, double unit_overhead, int64_t max_S,
                 Plan &p, bool whole_blocks = false) {
@@ -346,6 +353,26 @@ bool bf16_r64_enabled(int64_t k, int64_t n, int64_t d) {
 // compute = PMM_COMPUTE_F32: the f32 kernel (variant chosen by LDS fit);
 // PMM_COMPUTE_BF16: the wave-specialised bf16 kernel (variant -2, 128 x 64
 // tiles, 8 waves) or the 4-wave one (variant -1, 128 x 128 tiles).
+// Fire-and-forget 256-row bf16 kernel (pmm_bf16_ff_kernel.h): PMM_BF16_FF=1
+// (read per call).  Needs a corpus long enough for its guessed threshold: a
+// sample of ns_g <= n / 16 rows whose j-th best leaves about n j / ns_g >= 4 k
+// scores per row, N < 2^26, and a padded D the kernel's registers hold.
+int ff_guess_j() {
+  const char *e = getenv("PMM_FF_J");
+  return e ? std::max(1, atoi(e)) : 5;
+}
+int64_t ff_guess_ns(int64_t n) { return std::min<int64_t>(2048, (n / 16) / 32 * 32); }
+bool bf16_ff_enabled(int64_t k, int64_t n, int64_t d) {
+  const char *e = getenv("PMM_BF16_FF");
+  const int mode = e ? atoi(e) : 0;  // 2 (tests): whenever the kernel can run, however bad the guess
+  if (mode == 0) return false;
+  const int dp = (int)(cdiv(d, kBf16DAlign) * kBf16DAlign);
+  const int64_t ns = ff_guess_ns(n);
+  const bool guess_ok = (double)n * ff_guess_j() / (double)ns >= 4.0 * (double)k;
+  return ns >= 256 && ns >= ff_guess_j() && (guess_ok || mode == 2) && k + 64 <= 8192 && n < (1 << 26) &&
+         gemm_bf16_ff_lds_bytes(dp) > 0 && gemm_bf16_ff_lds_bytes(dp) <= 160 * 1024;
+}
+
 int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p,
               int compute = PMM_COMPUTE_F32) {
   // testing knob: plan for fewer workgroups (small problems then take the
@@ -368,12 +395,13 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
     if (cap_env > 0 && k + 64 <= 512) p.capg = std::max<int>(((int)k + 64 + 7) / 8 * 8, std::min(cap_env, 512) / 8 * 8);
   }
   const bool bf16 = compute == PMM_COMPUTE_BF16;
-  const bool r64 = bf16 && bf16_r64_enabled(k, n, d);
+  const bool ffk = bf16 && !t_no_ff && bf16_ff_enabled(k, n, d);
+  const bool r64 = bf16 && !ffk && bf16_r64_enabled(k, n, d);
   if (r64) p.capg = next_pow2((int)k + 64, 128);  // (its compaction: 4 keys per lane)
-  const bool ws = bf16 && !r64 && bf16_ws_enabled(p.capg, d);
-  p.variant = bf16 ? (r64 ? -5 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
-  const int bm = bf16 ? (r64 ? kBf16R64BM : kBf16BM) : gemm_f32_bm(p.variant);
-  const int bn = bf16 ? (r64 ? kBf16R64BN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
+  const bool ws = bf16 && !ffk && !r64 && bf16_ws_enabled(p.capg, d);
+  p.variant = bf16 ? (ffk ? -6 : r64 ? -5 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
+  const int bm = bf16 ? (ffk ? kBf16FfBM : r64 ? kBf16R64BM : kBf16BM) : gemm_f32_bm(p.variant);
+  const int bn = bf16 ? (ffk ? kBf16FfBN : r64 ? kBf16R64BN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
   const size_t cand_budget = size_t(8) << 30;
   int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
@@ -390,12 +418,26 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   // f32 kernel: the same split of units (PMM_F32_WHOLE=0: split units only).
   // At c3 the GEMM time is unchanged (1076 ms either way) and the merge reads
   // 0.89 GB instead of 2.17 GB (0.40 vs 0.65 ms).
-  const bool whole = bf16 ? ((ws || r64) && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
+  const bool whole = bf16 ? ((ws || r64) && !ffk && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
   // unit overhead in tiles: loading the unit's query rows into registers
   // (Two 128 x 128 f32 workgroups per CU -- 196 registers and 74 KiB of LDS
   // let them co-reside -- planned for 512 slots measured slower at c1: 0.129
   // vs 0.118 ms, profiles/r3_c1/wpc_variant_ab.txt.)
-  plan_units(m, n, bm, bn, cus, bf16 ? (r64 ? 8.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
+  plan_units(m, n, bm, bn, cus, bf16 ? (ffk || r64 ? 8.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
+  if (ffk) {
+    // expected survivors of the guessed threshold per row, n j / ns, and per
+    // (row, split); a row's count varies with the sample's j-th (a Gamma(j)
+    // quantile: 3x the mean is rare), a region's (64 rows) much less
+    p.ff_ns = (int)ff_guess_ns(n);
+    p.ff_j = ff_guess_j();
+    const double e_row = (double)n * p.ff_j / p.ff_ns;
+    const double e_rs = e_row * std::min<double>(1.0, (double)p.tps * bn / (double)n);
+    p.capg = (int)std::max<int64_t>(k + 64, ((int64_t)(3.0 * e_rs) + 64 + 63) / 64 * 64);
+    // (the seed's sample of ns scores per row lives in the candidate lists)
+    p.capg = (int)std::max<int64_t>(p.capg, cdiv((int64_t)p.ff_ns, 2 * p.S));
+    p.ffcap = (int)(((int64_t)(1.5 * 64.0 * e_rs) + 256 + 63) / 64 * 64);
+    if (const char *ce = getenv("PMM_FF_CAP")) p.ffcap = std::max(64, atoi(ce));  // (tests: force overflows)
+  }
   // merge_kernel's per-row LDS capacity: at least 512, so a row's candidate
   // lists rarely need a compaction before the final one (c1: ~400 survivors
   // of the seed threshold per row; P = 128 compacted ~6 times, 23 us)
@@ -415,6 +457,14 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   off = al256(off + (metric != kMetricDot ? (size_t)n * 8 : 0));
   p.off_wq = off;  // f32 kernel: per-wave survivor queues, grid x waves x (32 x BN) u64
   off = al256(off + (bf16 ? 0 : (size_t)p.grid * (bm / 32) * 32 * bn * 8));
+  if (ffk) {
+    p.off_ffcnt = off;  // [units][4 waves]
+    off = al256(off + (size_t)p.units * 4 * 4);
+    p.off_ffreg = off;  // [units][4 waves][ffcap]
+    off = al256(off + (size_t)p.units * 4 * p.ffcap * 8);
+    p.off_fb = off;  // [count | rows m]
+    off = al256(off + 16 + (size_t)m * 4);
+  }
   p.total = off;
   (void)d;
   return PMM_OK;
@@ -744,6 +794,10 @@ int bf16_limits(int64_t d, int64_t k, int64_t n) {
   return PMM_OK;
 }
 
+int ff_rerun(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c, int64_t ldc, int64_t n, int64_t d,
+             int64_t k, int metric, uint32_t index_base, uint32_t *out_idx, float *out_score, const unsigned *fb,
+             hipStream_t s, int dev);
+
 int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c,
                           int64_t ldc, int64_t n, int64_t d, int64_t k, int metric,
                           uint32_t index_base, uint32_t *out_idx, float *out_score, void *ws,
@@ -841,7 +895,31 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
         HIP_TRY(launch_seed_select(sample, ns, (int)m, (int)ns, (int)k, metric, a.gthr, s));
       }
     }
-    {
+    if (p.variant == -6) {
+      // fire-and-forget 256-row kernel: the guessed threshold (the j-th best
+      // of an exact ns-row sample, minus 1), the pass, the exact re-score and
+      // bucketing into the candidate lists; rows it cannot prove exact are
+      // re-run below
+      float *sample = (float *)(w + p.off_cand);
+      {
+        Timed t("seed_bf16", s);
+        HIP_TRY(launch_seed_bf16_ws(a, sample, p.ff_ns, s));
+        HIP_TRY(launch_seed_select(sample, p.ff_ns, (int)m, p.ff_ns, p.ff_j, metric, a.gthr, s));
+      }
+      a.qb_full = 0;
+      a.ffreg = (unsigned long long *)(w + p.off_ffreg);
+      a.ffcnt = (unsigned *)(w + p.off_ffcnt);
+      a.ffcap = p.ffcap;
+      {
+        Timed t("gemm_bf16_topk/ff", s);
+        HIP_TRY(launch_gemm_bf16_ff(a, p.grid, s));
+      }
+      HIP_TRY(hipMemsetAsync(w + p.off_fb, 0, 16, s));
+      {
+        Timed t("ff_bucket", s);
+        HIP_TRY(launch_ff_bucket(a, (unsigned *)(w + p.off_fb), (int *)(w + p.off_fb + 16), s));
+      }
+    } else {
       // (the suffix names the kernel; pmm_timing_read matches substrings)
       Timed t(p.variant == -5   ? "gemm_bf16_topk/r64"
               : p.variant == -2 ? "gemm_bf16_topk/ws"
@@ -889,7 +967,68 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     Timed t("merge_topk", s);
     HIP_TRY(launch_merge(ma, 0, s));
   }
+  if (p.variant == -6) {
+    int rc = ff_rerun(q, ldq, m, c, ldc, n, d, k, metric, index_base, out_idx, out_score,
+                      (const unsigned *)(w + p.off_fb), s, dev);
+    if (rc) return rc;
+  }
   return own ? arena_record(dev, s) : PMM_OK;
+}
+
+// The fire-and-forget kernel's rows that it could not prove exact (fewer than
+// k candidates at or above the guessed threshold, or a dropped survivor):
+// their query rows are gathered and re-run on the wave-specialised kernel
+// against the whole corpus, and their lists replace the merge's.  Reads the
+// row count back (a stream synchronisation); rare: the guess leaves about
+// n j / ns scores per row against the k needed.
+int ff_rerun(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c, int64_t ldc, int64_t n, int64_t d,
+             int64_t k, int metric, uint32_t index_base, uint32_t *out_idx, float *out_score, const unsigned *fb,
+             hipStream_t s, int dev) {
+  unsigned nfb = 0;
+  HIP_TRY(hipMemcpyAsync(&nfb, fb, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (nfb == 0) return PMM_OK;
+  std::vector<int> rows(nfb);
+  HIP_TRY(hipMemcpyAsync(rows.data(), fb + 4, (size_t)nfb * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const int64_t r = nfb;
+  uint16_t *qs = nullptr;
+  uint32_t *oi = nullptr;
+  float *os = nullptr;
+  void *wsb = nullptr;
+  struct Free {
+    void *p[4];
+    ~Free() {
+      for (void *x : p)
+        if (x) (void)hipFree(x);
+    }
+  } fr{{nullptr, nullptr, nullptr, nullptr}};
+  const bool prev = t_no_ff;
+  t_no_ff = true;
+  const int64_t dp = cdiv(d, kBf16DAlign) * kBf16DAlign;
+  const size_t wb = pmm_topk_workspace_bytes(r, n, dp, k, metric, PMM_COMPUTE_BF16);
+  hipError_t e = hipMalloc(&qs, (size_t)r * ldq * 2);
+  fr.p[0] = qs;
+  if (e == hipSuccess) e = hipMalloc(&oi, (size_t)r * k * 4);
+  fr.p[1] = oi;
+  if (e == hipSuccess) e = hipMalloc(&os, (size_t)r * k * 4);
+  fr.p[2] = os;
+  if (e == hipSuccess) e = hipMalloc(&wsb, wb);
+  fr.p[3] = wsb;
+  for (int64_t i = 0; i < r && e == hipSuccess; i++)
+    e = hipMemcpyAsync(qs + i * ldq, q + (int64_t)rows[i] * ldq, (size_t)ldq * 2, hipMemcpyDeviceToDevice, s);
+  int rc = PMM_OK;
+  if (e == hipSuccess)
+    rc = topk_bf16_device_impl(qs, ldq, r, c, ldc, n, d, k, metric, index_base, oi, os, wsb, wb, s, dev);
+  t_no_ff = prev;
+  if (e != hipSuccess) return fail(PMM_ERR_HIP, "ff re-run: %s", hipGetErrorString(e));
+  if (rc) return rc;
+  for (int64_t i = 0; i < r; i++) {
+    HIP_TRY(hipMemcpyAsync(out_idx + (int64_t)rows[i] * k, oi + i * k, (size_t)k * 4, hipMemcpyDeviceToDevice, s));
+    HIP_TRY(hipMemcpyAsync(out_score + (int64_t)rows[i] * k, os + i * k, (size_t)k * 4, hipMemcpyDeviceToDevice, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));  // (before the buffers are freed)
+  return PMM_OK;
 }
 
 // Upload a host matrix rows x d into a device buffer with row stride dp,

@@ -60,6 +60,12 @@ struct GemmF32Args {
   int qb_full;                    // wave-specialised bf16 kernel: query blocks processed whole
                                   // (phase A; a multiple of the grid), the rest as split units
   unsigned long long *stats;      // PMM_STATS only: [queued, flagged groups, tiles, compactions]
+  // fire-and-forget bf16 kernel (pmm_bf16_ff_kernel.h): per-(unit, wave)
+  // survivor regions of ffcap items (raw dot | row << 58 | column << 32) and
+  // their counts (a count above ffcap: the region overflowed)
+  unsigned long long *ffreg;
+  unsigned *ffcnt;
+  int ffcap;
 };
 
 struct MergeArgs {
@@ -157,6 +163,18 @@ constexpr int kBf16R64BM = 256, kBf16R64BN = 32;
 constexpr int kBf16R64MaxCapg = 256;  // its compaction holds 4 keys per lane (k <= 192)
 size_t gemm_bf16_r64_lds_bytes(int D);  // D = padded dimension; 0 if unsupported
 hipError_t launch_gemm_bf16_r64(const GemmF32Args &a, int grid, hipStream_t s);
+// 256-query-row bf16 kernel on v_mfma_f32_16x16x32_bf16 with survivors stored
+// fire-and-forget against a static guessed threshold (pmm_bf16_ff_kernel.h):
+// 64 rows x D per wave, 32-column corpus tiles.  N < 2^26.
+constexpr int kBf16FfBM = 256, kBf16FfBN = 32;
+size_t gemm_bf16_ff_lds_bytes(int D);  // D = padded dimension; 0 if unsupported
+hipError_t launch_gemm_bf16_ff(const GemmF32Args &a, int grid, hipStream_t s);
+// Exact re-score and bucketing of the ff kernel's survivor regions into the
+// per-(row, split) candidate lists of merge_kernel: one workgroup per (query
+// block, wave); rows whose lists overflowed, whose region overflowed or that
+// kept fewer than k candidates at or above their threshold go to fb_rows
+// (*fb_count of them) for a re-run.
+hipError_t launch_ff_bucket(const GemmF32Args &a, unsigned *fb_count, int *fb_rows, hipStream_t s);
 // f32 rows -> bf16 (round to nearest even) with row stride ldd, columns
 // d..ldd-1 zero-filled.
 hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t lds, uint16_t *dst,

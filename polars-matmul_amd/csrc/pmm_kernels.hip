@@ -901,11 +901,13 @@ __global__ __launch_bounds__(256) void seed_select_kernel(const float *__restric
 hipError_t launch_seed_select(const float *S, int64_t lds, int m, int ns, int k, int metric,
                               unsigned long long *gthr, hipStream_t s) {
   if (m <= 0) return hipSuccess;
-  if (ns > kSeedMaxNs || k > ns) return hipErrorInvalidValue;
+  // (up to 2048: the fire-and-forget bf16 kernel's guess sample)
+  if (ns > 2048 || k > ns) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((m + 3) / 4);
   if (ns <= 256) seed_select_kernel<4><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
   else if (ns <= 512) seed_select_kernel<8><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
-  else seed_select_kernel<16><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
+  else if (ns <= 1024) seed_select_kernel<16><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
+  else seed_select_kernel<32><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
   return hipGetLastError();
 }
 
@@ -1229,10 +1231,12 @@ hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const floa
   a.z1 = (uint4 *)z1;
   a.z0n = (int64_t)(z0_bytes / 16);
   a.z1n = (int64_t)(z1_bytes / 16);
-  // MFMA seed blocks (seed_mfma_block) when the sample's keys fit LDS
-  // (PMM_SEED_MFMA=0, read per call: the fmaf-chain seed blocks)
+  // MFMA seed blocks (seed_mfma_block) only on request (PMM_SEED_MFMA=1, read
+  // per call) and when the sample's keys fit LDS: 32 blocks of 4 waves at c1
+  // walk their tiles one after another, latency-bound -- prologue 79 us
+  // against the fmaf-chain seed's 21 (c2: 43 vs 17; gpurun_out r4c, same box)
   const char *sme = getenv("PMM_SEED_MFMA");
-  a.mfma_seed = (ns % 32 == 0 && ns <= 512 && !(sme && atoi(sme) == 0)) ? 1 : 0;
+  a.mfma_seed = (ns % 32 == 0 && ns <= 512 && sme && atoi(sme) == 1) ? 1 : 0;
   a.sblocks = a.mfma_seed ? (unsigned)((m + 31) / 32) : (unsigned)((m + seedk::RQ - 1) / seedk::RQ);
   const bool xf = metric != kMetricDot;
   a.qblocks = xf ? (unsigned)((m * 8 + 255) / 256) : 0u;

@@ -15,14 +15,15 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
 
 # (source, defines): every padded-D instantiation of the wave-specialised
 # kernel, the ring sizes whose slot sequence repeats per tile, the
-# one-wave-per-SIMD bf16 kernel at the largest D and every instantiation of
-# the 256-row one-wave kernel (lab build)
+# one-wave-per-SIMD bf16 kernel at the largest D, every instantiation of the
+# 256-row one-wave kernel (lab build) and of the fire-and-forget 256-row one
 BUILDS = [("pmm_bf16_ws_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
     ("pmm_bf16_ws_ks.hip", ("-DPMM_BF16_KS=6", "-DPMM_WS_NST=6")),
     ("pmm_bf16_ws_ks.hip", ("-DPMM_BF16_KS=6", "-DPMM_WS_NST=3")),
     ("pmm_bf16_ks.hip", ("-DPMM_BF16_KS=6",)),
 ] + [
-    ("pmm_bf16_r64_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)]
+    ("pmm_bf16_r64_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
+    ("pmm_bf16_ff_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)]
 
 
 def have_hipcc():

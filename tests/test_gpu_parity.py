@@ -922,7 +922,7 @@ def test_threshold_seeding_changes_nothing(pmm, k, d, monkeypatch):
         monkeypatch.setenv("PMM_SEED_GEMM", "1")
         got_g = gpu_topk(q, c, k, metric)
         monkeypatch.delenv("PMM_SEED_GEMM")
-        monkeypatch.setenv("PMM_SEED_MFMA", "0")  # the fmaf-chain seed blocks
+        monkeypatch.setenv("PMM_SEED_MFMA", "1")  # the MFMA seed blocks (opt-in)
         got_f = gpu_topk(q, c, k, metric)
         monkeypatch.delenv("PMM_SEED_MFMA")
         monkeypatch.delenv("PMM_SEED")
@@ -1239,6 +1239,84 @@ def test_bf16_r64_seeded_1m_rows_equal_ws(pmm, lab, monkeypatch):
         outs.append((oi.cpu().numpy(), osc.cpu().numpy()))
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
+
+
+# ---- the fire-and-forget 256-row bf16 kernel (pmm_bf16_ff_kernel.h,
+# PMM_BF16_FF=1): 16x16x32 MFMAs (a different f32 summation grouping than the
+# wave-specialised kernel's 32x32x16), a guessed static threshold, survivors
+# re-scored exactly and bucketed afterwards, rows it cannot prove exact re-run
+# on the wave-specialised kernel.  Every list passes the bf16 truth check
+# (the exact top-k of the rounded rows up to f32 summation order) and agrees
+# with the wave-specialised kernel but for near-ties ----
+@pytest.mark.parametrize("m,n,d,k", [(300, 70000, 256, 10), (520, 200000, 768, 100), (257, 131072, 384, 32),
+                                     (1000, 100003, 128, 20), (70, 90000, 640, 8), (33, 66000, 500, 16)])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_ff_vs_truth_and_ws(pmm, m, n, d, k, metric, monkeypatch):
+    rs = np.random.RandomState(m + n + d + k + 13)
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    c[n // 2:n // 2 + 20] = c[:20]  # exact ties across the corpus
+    q[m // 2] = 0.0                  # a zero-norm query row
+    monkeypatch.setenv("PMM_BF16_FF", "1")
+    fi, fsc = gpu_topk_bf16(q, c, k, metric)
+    _bf16_truth_check(q, c, k, metric, fi, fsc, f"bf16 ff {m}x{n}x{d} k={k} {metric}")
+    monkeypatch.setenv("PMM_BF16_FF", "0")
+    wi, wsc = gpu_topk_bf16(q, c, k, metric)
+    assert float(np.mean(fi == wi)) > 0.98
+    assert np.max(np.abs(fsc.astype(np.float64) - wsc)) < 1e-4 * max(1.0, float(np.max(np.abs(wsc))))
+
+
+@pytest.mark.parametrize("knobs", [{"PMM_FF_J": "1"}, {"PMM_FF_CAP": "256"}, {"PMM_FF_J": "1", "PMM_FF_CAP": "64"}])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_bf16_ff_reruns_rows_it_cannot_prove(pmm, knobs, metric, monkeypatch):
+    # a guess at the sample's best (j = 1: about n / ns scores per row pass,
+    # fewer than k for many rows) and/or survivor regions far too small
+    # (dropped items): the affected rows must be re-run, and every list must
+    # still be the exact top-k of the rounded rows
+    rs = np.random.RandomState(71 + len(knobs) + METRICS[metric])
+    m, n, d, k = 400, 70000, 256, 60
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    monkeypatch.setenv("PMM_BF16_FF", "2")  # forced, whatever the guess leaves
+    for kk, v in knobs.items():
+        monkeypatch.setenv(kk, v)
+    fi, fsc = gpu_topk_bf16(q, c, k, metric)
+    _bf16_truth_check(q, c, k, metric, fi, fsc, f"bf16 ff rerun {knobs} {metric}")
+    for kk in knobs:
+        monkeypatch.delenv(kk)
+    monkeypatch.setenv("PMM_BF16_FF", "0")
+    wi, _ = gpu_topk_bf16(q, c, k, metric)
+    assert float(np.mean(fi == wi)) > 0.98
+
+
+def test_bf16_ff_device_api_whole_problem(pmm, monkeypatch):
+    # the device entry point at a size with several splits per query block:
+    # every row vs float64 truth on device, indices distinct
+    import torch
+
+    monkeypatch.setenv("PMM_BF16_FF", "1")
+    n = _native()
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(37)
+    m, N, d, k = 3000, 400000, 768, 100
+    q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
+    c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
+    oi = torch.empty((m, k), dtype=torch.int32, device=dev)
+    osc = torch.empty((m, k), dtype=torch.float32, device=dev)
+    n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS["cosine"],
+                       oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    qd, cd = q.double(), c.double()
+    s = (qd @ cd.T) / (qd.norm(dim=1, keepdim=True) * cd.norm(dim=1)[None, :])
+    ref_s, _ = torch.topk(s, k, dim=1)
+    got_true = torch.gather(s, 1, oi.long())
+    kth = ref_s[:, -1:]
+    ok = got_true >= kth - (1e-5 * kth.abs() + 1e-5)
+    assert bool(ok.all()), float(ok.float().mean())
+    assert float((osc.double() - got_true).abs().max()) < 1e-4
+    srt = torch.sort(oi, dim=1).values
+    assert bool((srt[:, 1:] != srt[:, :-1]).all())
 
 
 @pytest.mark.parametrize("m", [33, 300])

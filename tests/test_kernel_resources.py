@@ -37,7 +37,7 @@ def compiler_m0_uses(asm: str):
             inasm = False
             continue
         s = line.strip()
-        if not inasm and func and "r64" in func and not s.startswith(";") and re.search(r"\bm0\b", s):
+        if not inasm and func and ("r64" in func or "_ff_" in func) and not s.startswith(";") and re.search(r"\bm0\b", s):
             out.append((func, s))
     return out
 
