@@ -218,6 +218,7 @@ hipError_t launch_gemm_f64_topk(const F64TopkArgs &a, hipStream_t s) {
 // A count above the capacity means entries were dropped: *overflow is set and
 // the host discards the result.
 // ---------------------------------------------------------------------------
+constexpr int kF64SelE = 16;  // selection path: buffers of up to 1024 entries in registers
 __global__ __launch_bounds__(256) void f64_select_kernel(F64SelArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -230,8 +231,80 @@ __global__ __launch_bounds__(256) void f64_select_kernel(F64SelArgs a) {
     if (lane == 0) atomicOr(a.overflow, 1u);
     n = a.cap;
   }
-  const int P2 = min(a.P, next_pow2_dev(n));
   const Ent* src = a.cand + (int64_t)row * a.cap;
+  if (n > a.k && n <= 64 * kF64SelE) {
+    // Selection instead of a sort of the whole buffer: the k-th key by
+    // ballots (wave_kth_u64, the value with multiplicity), then among the
+    // entries tied at it the (k - #greater)-th smallest index.  The kept set
+    // {key > tk} + {key == tk, idx <= tx} is exactly the sort's first k.
+    // NaN scores (key 0) outnumbering n - k fall through to the sort.
+    u64 x[kF64SelE];
+    uint32_t ix[kF64SelE];
+#pragma unroll
+    for (int e = 0; e < kF64SelE; e++) {
+      const int j = lane + 64 * e;
+      x[e] = 0ull;
+      ix[e] = 0xFFFFFFFFu;
+      if (j < n) {
+        const Ent en = src[j];
+        x[e] = en.key;
+        ix[e] = en.idx;
+      }
+    }
+    int nz = 0;
+#pragma unroll
+    for (int e = 0; e < kF64SelE; e++) nz += __popcll(__ballot(x[e] != 0ull));
+    if (nz >= a.k) {
+      const u64 tk = wave_kth_u64<kF64SelE>(x, a.k);
+      int gt = 0;
+#pragma unroll
+      for (int e = 0; e < kF64SelE; e++) gt += __popcll(__ballot(x[e] > tk));
+      u64 y[kF64SelE];
+#pragma unroll
+      for (int e = 0; e < kF64SelE; e++) y[e] = x[e] == tk ? (u64)(~ix[e]) : 0ull;
+      const uint32_t tx = ~(uint32_t)wave_kth_u64<kF64SelE>(y, a.k - gt);
+      Ent *dst = a.mode == 0 ? a.cand + (int64_t)row * a.cap : scr;
+      int base = 0;
+#pragma unroll
+      for (int e = 0; e < kF64SelE; e++) {
+        const bool keep = x[e] > tk || (x[e] == tk && ix[e] <= tx);
+        const u64 msk = __ballot(keep);
+        if (keep) {
+          Ent en;
+          en.key = x[e];
+          en.idx = ix[e];
+          en.pad = 0u;
+          dst[base + lanes_below(msk)] = en;
+        }
+        base += __popcll(msk);
+      }
+      if (a.mode == 0) {
+        if (lane == 0) {
+          a.cnt[row] = (unsigned)a.k;
+          a.tkey[row] = tk;
+          a.tidx[row] = tx;
+        }
+        return;
+      }
+      // final: sort the k kept entries only
+      const int P2 = next_pow2_dev(a.k);
+      for (int j = a.k + lane; j < P2; j += 64) {
+        Ent e;
+        e.key = 0ull;
+        e.idx = 0xFFFFFFFFu;
+        e.pad = 0u;
+        scr[j] = e;
+      }
+      wave_sync();
+      wave_sort_desc_ent(scr, P2, lane);
+      for (int j = lane; j < a.k; j += 64) {
+        a.out_idx[(int64_t)row * a.k + j] = scr[j].idx + a.index_base;
+        a.out_score[(int64_t)row * a.k + j] = f64_unkey(scr[j].key, a.metric);
+      }
+      return;
+    }
+  }
+  const int P2 = min(a.P, next_pow2_dev(n));
   for (int j = lane; j < P2; j += 64) {
     Ent e;
     if (j < n) {
