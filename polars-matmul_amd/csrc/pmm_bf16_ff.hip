@@ -114,8 +114,21 @@ __global__ __launch_bounds__(256) void ff_bucket_kernel(GemmF32Args a, unsigned 
 hipError_t launch_ff_bucket(const GemmF32Args &a, unsigned *fb_count, int *fb_rows, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
   const unsigned grid = (unsigned)(a.QB * ff::NW);
+  // (many splits per query block -- few query rows over a long corpus -- take
+  // more than the default 64 KiB of counters)
   const size_t lds = (size_t)64 * a.S * 4 + 64 * 4;
-  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > 64 * 1024) {
+    static bool attr_set[3] = {false, false, false};
+    if (!attr_set[a.metric]) {
+      const void *fn = a.metric == kMetricCosine ? (const void *)ff_bucket_kernel<kMetricCosine>
+                       : a.metric == kMetricDot  ? (const void *)ff_bucket_kernel<kMetricDot>
+                                                 : (const void *)ff_bucket_kernel<kMetricEuclidean>;
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+      attr_set[a.metric] = true;
+    }
+  }
   if (a.metric == kMetricCosine) ff_bucket_kernel<kMetricCosine><<<grid, 256, lds, s>>>(a, fb_count, fb_rows);
   else if (a.metric == kMetricDot) ff_bucket_kernel<kMetricDot><<<grid, 256, lds, s>>>(a, fb_count, fb_rows);
   else ff_bucket_kernel<kMetricEuclidean><<<grid, 256, lds, s>>>(a, fb_count, fb_rows);
