@@ -595,19 +595,22 @@ def kernel_stats(bf16):
 
     names = {"gemm": "gemm_bf16_topk" if bf16 else "gemm_f32_topk",
              "seed": "seed_bf16" if bf16 else "gemm_f32_seed",
-             "merge": "merge_topk", "shard_merge": "merge_shards", "norms": "norms_"}
+             "merge": "merge_topk", "shard_merge": "merge_shards", "norms": "norms_",
+             "ff_bucket": "ff_bucket"}
     out = {}
     for key, nm in names.items():
         ms, n = _native.timing_read(nm)
         out[key] = (ms / n if n else None, n)
     if bf16:
         # which bf16 kernel ran (the library's timer names carry it)
-        out["bf16_kernel"] = next((v for v in ("r64", "ws", "one-wave")
+        out["bf16_kernel"] = next((v for v in ("ff", "r64", "ws", "one-wave")
                                    if _native.timing_read("gemm_bf16_topk/" + v)[1]), "ws")
     return out
 
 
 BF16_KERNEL_NAMES = {
+    "ff": "gemm_bf16_ff_kernel (256 query rows per CU on 16x16x32 MFMAs, pre-filter against a guessed "
+          "static threshold, survivors stored fire-and-forget; + seed_bf16_ws_kernel in achieved)",
     "r64": "gemm_bf16_r64_kernel (256 query rows held by one wave per SIMD: fused GEMM + metric + top-k; "
            "+ seed_bf16_ws_kernel in achieved)",
     "ws": "gemm_bf16_ws_kernel (wave-specialised fused GEMM + metric + top-k; "
@@ -716,6 +719,8 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8, stride=1)
         "shard_merge_ms_avg": round(ks["shard_merge"][0], 3) if ks["shard_merge"][0] else None,
         "norms_ms_avg": round(ks["norms"][0], 3) if ks["norms"][0] else None,
     }
+    if ks["ff_bucket"][1]:
+        roof["ff_bucket_ms_avg"] = round(ks["ff_bucket"][0], 3)
     reduction = None
     if ks["merge"][1] and merge_bytes:
         mavg = ks["merge"][0] / 1000.0

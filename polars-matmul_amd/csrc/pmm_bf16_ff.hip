@@ -135,4 +135,40 @@ hipError_t launch_ff_bucket(const GemmF32Args &a, unsigned *fb_count, int *fb_ro
   return hipGetLastError();
 }
 
+// The re-run's row gather (query rows listed in rows[0..r) into a dense
+// block) and list scatter (the re-run's lists back to those rows).
+__global__ __launch_bounds__(256) void ff_gather_rows_kernel(const uint16_t *__restrict__ q, int64_t ldq,
+                                                             const int *__restrict__ rows, int r,
+                                                             uint16_t *__restrict__ dst) {
+  const int i = blockIdx.x;
+  if (i >= r) return;
+  const uint16_t *src = q + (int64_t)rows[i] * ldq;
+  for (int64_t j = threadIdx.x; j < ldq; j += 256) dst[(int64_t)i * ldq + j] = src[j];
+}
+__global__ __launch_bounds__(256) void ff_scatter_lists_kernel(const uint32_t *__restrict__ oi,
+                                                               const float *__restrict__ os,
+                                                               const int *__restrict__ rows, int r, int k,
+                                                               uint32_t *__restrict__ out_idx,
+                                                               float *__restrict__ out_score) {
+  const int i = blockIdx.x;
+  if (i >= r) return;
+  const int64_t row = rows[i];
+  for (int j = threadIdx.x; j < k; j += 256) {
+    out_idx[row * k + j] = oi[(int64_t)i * k + j];
+    out_score[row * k + j] = os[(int64_t)i * k + j];
+  }
+}
+hipError_t launch_ff_gather_rows(const uint16_t *q, int64_t ldq, const int *rows, int r, uint16_t *dst,
+                                 hipStream_t s) {
+  if (r <= 0) return hipSuccess;
+  ff_gather_rows_kernel<<<r, 256, 0, s>>>(q, ldq, rows, r, dst);
+  return hipGetLastError();
+}
+hipError_t launch_ff_scatter_lists(const uint32_t *oi, const float *os, const int *rows, int r, int k,
+                                   uint32_t *out_idx, float *out_score, hipStream_t s) {
+  if (r <= 0) return hipSuccess;
+  ff_scatter_lists_kernel<<<r, 256, 0, s>>>(oi, os, rows, r, k, out_idx, out_score);
+  return hipGetLastError();
+}
+
 }  // namespace pmm

@@ -987,48 +987,36 @@ int ff_rerun(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c, int64
   unsigned nfb = 0;
   HIP_TRY(hipMemcpyAsync(&nfb, fb, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (getenv("PMM_FF_DEBUG")) fprintf(stderr, "[pmm ff] re-run rows %u of %lld\n", nfb, (long long)m);
   if (nfb == 0) return PMM_OK;
-  std::vector<int> rows(nfb);
-  HIP_TRY(hipMemcpyAsync(rows.data(), fb + 4, (size_t)nfb * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  // one allocation: the gathered rows, their lists, the re-run's workspace;
+  // the row list stays on the device (gather and scatter kernels read it)
   const int64_t r = nfb;
-  uint16_t *qs = nullptr;
-  uint32_t *oi = nullptr;
-  float *os = nullptr;
-  void *wsb = nullptr;
-  struct Free {
-    void *p[4];
-    ~Free() {
-      for (void *x : p)
-        if (x) (void)hipFree(x);
-    }
-  } fr{{nullptr, nullptr, nullptr, nullptr}};
+  const int *rows = (const int *)(fb + 4);
   const bool prev = t_no_ff;
   t_no_ff = true;
   const int64_t dp = cdiv(d, kBf16DAlign) * kBf16DAlign;
   const size_t wb = pmm_topk_workspace_bytes(r, n, dp, k, metric, PMM_COMPUTE_BF16);
-  hipError_t e = hipMalloc(&qs, (size_t)r * ldq * 2);
-  fr.p[0] = qs;
-  if (e == hipSuccess) e = hipMalloc(&oi, (size_t)r * k * 4);
-  fr.p[1] = oi;
-  if (e == hipSuccess) e = hipMalloc(&os, (size_t)r * k * 4);
-  fr.p[2] = os;
-  if (e == hipSuccess) e = hipMalloc(&wsb, wb);
-  fr.p[3] = wsb;
-  for (int64_t i = 0; i < r && e == hipSuccess; i++)
-    e = hipMemcpyAsync(qs + i * ldq, q + (int64_t)rows[i] * ldq, (size_t)ldq * 2, hipMemcpyDeviceToDevice, s);
+  const size_t o_i = al256((size_t)r * ldq * 2), o_s = o_i + al256((size_t)r * k * 4),
+               o_w = o_s + al256((size_t)r * k * 4);
+  char *buf = nullptr;
+  hipError_t e = hipMalloc(&buf, o_w + wb);
   int rc = PMM_OK;
+  if (e == hipSuccess) e = launch_ff_gather_rows(q, ldq, rows, (int)r, (uint16_t *)buf, s);
   if (e == hipSuccess)
-    rc = topk_bf16_device_impl(qs, ldq, r, c, ldc, n, d, k, metric, index_base, oi, os, wsb, wb, s, dev);
+    rc = topk_bf16_device_impl((const uint16_t *)buf, ldq, r, c, ldc, n, d, k, metric, index_base,
+                               (uint32_t *)(buf + o_i), (float *)(buf + o_s), buf + o_w, wb, s, dev);
+  if (e == hipSuccess && rc == PMM_OK)
+    e = launch_ff_scatter_lists((const uint32_t *)(buf + o_i), (const float *)(buf + o_s), rows, (int)r, (int)k,
+                                out_idx, out_score, s);
   t_no_ff = prev;
-  if (e != hipSuccess) return fail(PMM_ERR_HIP, "ff re-run: %s", hipGetErrorString(e));
-  if (rc) return rc;
-  for (int64_t i = 0; i < r; i++) {
-    HIP_TRY(hipMemcpyAsync(out_idx + (int64_t)rows[i] * k, oi + i * k, (size_t)k * 4, hipMemcpyDeviceToDevice, s));
-    HIP_TRY(hipMemcpyAsync(out_score + (int64_t)rows[i] * k, os + i * k, (size_t)k * 4, hipMemcpyDeviceToDevice, s));
+  if (buf) {
+    const hipError_t e2 = hipStreamSynchronize(s);  // (before the buffer is freed)
+    (void)hipFree(buf);
+    if (e == hipSuccess) e = e2;
   }
-  HIP_TRY(hipStreamSynchronize(s));  // (before the buffers are freed)
-  return PMM_OK;
+  if (e != hipSuccess) return fail(PMM_ERR_HIP, "ff re-run: %s", hipGetErrorString(e));
+  return rc;
 }
 
 // Upload a host matrix rows x d into a device buffer with row stride dp,

@@ -218,7 +218,17 @@ __device__ __forceinline__ void norms_rows(const TI *__restrict__ a, int64_t row
   const int64_t d8 = d & ~(int64_t)7;
   T acc = (T)0;
   if (valid) {
-    for (int64_t i = j; i < d8; i += 8) {
+    // 8 loads in flight per lane (a plain loop waited for each: 32 exposed
+    // latencies per row at d = 256); the sum keeps its order
+    int64_t i = j;
+    for (; i + 56 < d8; i += 64) {
+      T x[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) x[u] = (T)p[i + 8 * u];
+#pragma unroll
+      for (int u = 0; u < 8; u++) acc = acc + x[u] * x[u];
+    }
+    for (; i < d8; i += 8) {
       const T x = (T)p[i];
       acc = acc + x * x;
     }

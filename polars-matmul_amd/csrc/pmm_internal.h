@@ -174,6 +174,10 @@ hipError_t launch_gemm_bf16_ff(const GemmF32Args &a, int grid, hipStream_t s);
 // block, wave); rows whose lists overflowed, whose region overflowed or that
 // kept fewer than k candidates at or above their threshold go to fb_rows
 // (*fb_count of them) for a re-run.
+hipError_t launch_ff_gather_rows(const uint16_t *q, int64_t ldq, const int *rows, int r, uint16_t *dst,
+                                 hipStream_t s);
+hipError_t launch_ff_scatter_lists(const uint32_t *oi, const float *os, const int *rows, int r, int k,
+                                   uint32_t *out_idx, float *out_score, hipStream_t s);
 hipError_t launch_ff_bucket(const GemmF32Args &a, unsigned *fb_count, int *fb_rows, hipStream_t s);
 // f32 rows -> bf16 (round to nearest even) with row stride ldd, columns
 // d..ldd-1 zero-filled.

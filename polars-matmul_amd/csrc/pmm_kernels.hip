@@ -945,111 +945,191 @@ struct PrologueArgs {
   uint4 *z0, *z1;              // zeroed ranges (16-byte words)
   int64_t z0n, z1n;
   unsigned sblocks, qblocks, cblocks, zblocks;
-  int mfma_seed;               // seed blocks of 32 rows on the f32 MFMA (seed_mfma_block)
+  int lds_seed;                // LDS-staged seed blocks (seed_lds_block)
+  int64_t cper;                // LDS-staged launch: corpus norm rows per block
 };
 
-// MFMA seed block: query rows 32 b .. 32 b + 31 against all ns sample columns
-// on v_mfma_f32_32x32x2_f32 -- the fused kernel's instruction with its
-// operand values in its order: substep t pairs k = 2t (lane half 0) with
-// 2t + 1 (half 1), from the first substep onto zeros, so every score is the
-// main pass's bit for bit.  Operands come straight from global memory as
-// 16-byte pieces (k = 8 j + 4 h .. + 3 on half h) and two v_permlane32_swap per
-// piece turn them into the natural-order pairs (the fused kernel's K order 1).
-// Wave w computes the 32 x 32 tiles of sample columns 32 (w + 4 i); the row
-// and column norms in ndarray order from the same rows (norms_rows), the
-// composite keys into LDS, then each wave selects 8 rows' k-th.  Against
-// seed_dots (4 rows per block, one sample column per thread as fmaf chains,
-// each thread streaming its own 1 KiB row: 19 us at c1, latency-bound) the
-// work is MFMA-paced: 128 MFMAs per tile at D = 256.
-template <int E, int METRIC>
-__device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned b, char *smem) {
-  constexpr bool XFORM = METRIC != kMetricDot;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r32 = lane & 31, h = lane >> 5;
-  const int ns = a.ns, dp = a.dp, NSP = 64 * E;
-  u64 *keys = (u64 *)smem;                        // [32][NSP]
-  float *qn_s = (float *)(smem + 32 * NSP * 8);   // [32]
-  float *cn_s = qn_s + 32;                        // [NSP]
-  const int row0 = (int)b * 32;
-  if (XFORM) {
-    norms_rows<float, float>(a.q + (int64_t)row0 * a.ldq, min(32, a.m - row0), a.d, a.ldq, a.squared, qn_s,
-                             nullptr, tid);
-    for (int g = tid; g < ns * 8; g += 256) norms_rows<float, float>(a.c, ns, a.d, a.ldc, a.squared, cn_s, nullptr, g);
-  }
-  const __amdgpu_buffer_rsrc_t ra =
-      make_rsrc(a.q + (int64_t)row0 * a.ldq, (int64_t)min(32, a.m - row0) * a.ldq * 4);
-  auto kpair = [](f32x4 &x) __attribute__((always_inline)) {
-    auto r0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[0]), __float_as_uint(x[1]), false, false);
-    auto r1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[2]), __float_as_uint(x[3]), false, false);
-    x[0] = __uint_as_float(r0[0]);
-    x[1] = __uint_as_float(r0[1]);
-    x[2] = __uint_as_float(r1[0]);
-    x[3] = __uint_as_float(r1[1]);
-  };
-  const uint32_t aoff = (uint32_t)(r32 * a.ldq * 4 + h * 16);
-  const int nj = dp / 8;
-  for (int ct = w; ct < ns / 32; ct += 4) {
-    const int col0 = ct * 32;
-    const __amdgpu_buffer_rsrc_t rb = make_rsrc(a.c + (int64_t)col0 * a.ldc, (int64_t)32 * a.ldc * 4);
-    const uint32_t boff = (uint32_t)(r32 * a.ldc * 4 + h * 16);
-    f32x16 acc = {};
-    constexpr int PD = 8;  // pieces in flight per operand
-    f32x4 ap[PD], bp[PD];
-#pragma unroll
-    for (int i = 0; i < PD; i++) {
-      const int j = min(i, nj - 1);
-      ap[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(aoff + j * 32), 0, 0));
-      bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (int)(boff + j * 32), 0, 0));
-    }
-    for (int j0 = 0; j0 < nj; j0 += PD) {
-#pragma unroll
-      for (int i = 0; i < PD; i++) {
-        if (j0 + i >= nj) break;  // (nj = dp / 8 is a multiple of 4, not of PD)
-        f32x4 av = ap[i], bv = bp[i];
-        const int jn = min(j0 + i + PD, nj - 1);
-        ap[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ra, (int)(aoff + jn * 32), 0, 0));
-        bp[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rb, (int)(boff + jn * 32), 0, 0));
-        kpair(av);
-        kpair(bv);
-#pragma unroll
-        for (int jj = 0; jj < 4; jj++) {
-          const int js = ((jj & 1) << 1) | (jj >> 1);  // swapped registers: {0, 2, 1, 3}
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[js], bv[js], acc, 0, 0, 0);
-        }
-      }
-    }
-    __syncthreads();  // (first tile: the norms in LDS; later: nothing, kept uniform)
-    const int col = col0 + r32;
-    const float cnv = XFORM ? cn_s[col] : 0.0f;
-#pragma unroll
-    for (int e = 0; e < 16; e++) {
-      const int r = acc_row(e, h);
-      u64 key = 0ull;
-      if (row0 + r < a.m) {
-        const float sc = exact_score<METRIC>(acc[e], XFORM ? qn_s[r] : 0.0f, cnv);
-        key = ((u64)okey32(METRIC == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~(uint32_t)col);
-      }
-      keys[r * NSP + col] = key;
-    }
-  }
-  for (int i = tid; i < 32 * NSP; i += 256)
-    if ((i % NSP) >= ns) keys[i] = 0ull;  // columns past the sample
-  __syncthreads();
-  for (int r = w * 8; r < w * 8 + 8; r++) {
-    if (row0 + r >= a.m) break;
-    u64 x[E];
-#pragma unroll
-    for (int e = 0; e < E; e++) x[e] = keys[r * NSP + lane + 64 * e];
-    const u64 th = wave_kth_u64<E>(x, a.k);
-    if (lane == 0) a.gthr[row0 + r] = th ? th - 1 : 0ull;
+// LDS-staged seed block (ns <= 256 sample columns, padded D <= 1024): the
+// arithmetic of the fmaf-chain block below, bit for bit (the same chains in
+// the same K order, the same norm accumulators), but the sample rows reach
+// the lanes through LDS.  The fmaf-chain block streams each lane's own 1 KiB
+// row: every load instruction touches 64 rows, so the vector cache's tag
+// lookups, not the bytes, set its 19-21 us at c1.  Here the block's 256
+// columns come in K chunks of 32 floats by LDS-DMA (one instruction: 8
+// columns x 128 contiguous bytes), through a 4-chunk ring with 3 chunks in
+// flight (asm DMA with counted vmcnt waits: hipcc would wait for the whole
+// ring at every LDS read), and each lane reads its column's chunk as eight
+// ds_read_b128 of 16-byte pieces XOR-swizzled by column (piece j of column c
+// in slot j ^ ((c >> 1) & 7): 16 lanes hit 16 distinct bank groups).
+// The block also writes its rows' query norms, and every block of the launch
+// takes a slice of the corpus norms and of the zero fill, so the launch has
+// no other block kinds (its 152 KiB of LDS admits one block per CU).
+namespace seedk {
+constexpr int KC = 32;               // K floats per ring chunk
+constexpr int NB = 4;                // ring chunks (NB - 1 in flight)
+constexpr int CHUNK = 256 * KC * 4;  // 256 columns: 32 KiB
+constexpr int kLdsMaxDp = 1024;
+__device__ __forceinline__ void wait_vm(int n) {
+  switch (n) {
+#define PMM_SEED_W(N) \
+  case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+    PMM_SEED_W(0) PMM_SEED_W(8) PMM_SEED_W(16) PMM_SEED_W(24)
+#undef PMM_SEED_W
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
-template <int E, int METRIC, int MFMA>
+// LDS-DMA of one 16-byte piece per lane into M0 + 16 lane (s_nop 4: M0's one
+// state, and five for any descriptor / offset SGPR fresh from a VALU write --
+// tests/test_asm_hazards.py)
+__device__ __forceinline__ void dma_b128(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff, uint32_t soff) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 4\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds" ::"s"(lds), "v"(voff),
+               "s"(r), "s"(soff)
+               : "memory");
+}
+}  // namespace seedk
+
+template <int METRIC>
+__device__ __forceinline__ void seed_lds_block(const PrologueArgs &a, unsigned b, char *smem) {
+  using namespace seedk;
+  constexpr bool XFORM = METRIC != kMetricDot;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dp = a.dp, d = a.d, ns = a.ns, m = a.m;
+  u64 *keys = (u64 *)(smem + NB * CHUNK);         // [RQ][256]
+  float *qs = (float *)(keys + RQ * 256);         // [RQ][dp]
+  float *qn_s = qs + RQ * dp;                     // [RQ]
+  const uint32_t ring_lds = (uint32_t)(size_t)(LDS_AS char *)smem;
+  const int row0 = b * RQ;
+  const int G = dp / KC;
+  // rows past the sample read as zeros (their keys are never used)
+  const __amdgpu_buffer_rsrc_t rc = make_rsrc(a.c, (int64_t)ns * a.ldc * 4);
+  // DMA instruction i of wave w fills slots (i 256 + tid): column 32 i +
+  // (tid >> 3), slot tid & 7, which holds K piece (tid & 7) ^ ((tid >> 4) & 7)
+  uint32_t voff = (uint32_t)((tid >> 3) * a.ldc * 4 + 16 * ((tid & 7) ^ ((tid >> 4) & 7)));
+  asm volatile("" : "+v"(voff));
+  const uint32_t colstep = (uint32_t)(32 * a.ldc * 4);
+  auto issue = [&](int g) __attribute__((always_inline)) {
+    const uint32_t dst = ring_lds + (uint32_t)((g % NB) * CHUNK + w * 64 * 16);
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      dma_b128(rc, __builtin_amdgcn_readfirstlane(dst + (uint32_t)(i * 256 * 16)), voff,
+               __builtin_amdgcn_readfirstlane((uint32_t)i * colstep + (uint32_t)(g * KC * 4)));
+  };
+  for (int g = 0; g < NB - 1 && g < G; g++) issue(g);
+  // the query rows, all loads in flight at once (dp / 4 <= 256: one piece
+  // per thread and row; the compiler's vmcnt wait for them also retires the
+  // ring's first chunks)
+  {
+    f32x4 v[RQ];
+    const bool on = tid < dp / 4;
+#pragma unroll
+    for (int r = 0; r < RQ; r++) {
+      v[r] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+      if (on && row0 + r < m) v[r] = *(const f32x4 *)(a.q + (int64_t)(row0 + r) * a.ldq + 4 * tid);
+    }
+#pragma unroll
+    for (int r = 0; r < RQ; r++)
+      if (on) *(f32x4 *)(qs + r * dp + 4 * tid) = v[r];
+  }
+  __syncthreads();
+  if (XFORM && w == 0) norms_rows<float, float>(qs, RQ, d, dp, a.squared, qn_s, nullptr, tid);
+  __syncthreads();
+  const int col = tid, d8 = d & ~7;
+  float acc[RQ];
+#pragma unroll
+  for (int r = 0; r < RQ; r++) acc[r] = 0.0f;
+  float p[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) p[j] = 0.0f;
+  const uint32_t rd0 = ring_lds + (uint32_t)(col * KC * 4);
+  const int swz = (col >> 1) & 7;
+  for (int g = 0; g < G; g++) {
+    // this wave's pieces of chunk g landed (younger: chunks g + 1 .. g + NB - 2)
+    wait_vm(8 * (min(G - 1, g + NB - 2) - g));
+    __builtin_amdgcn_s_barrier();  // everyone's pieces landed; everyone is past chunk g - 1
+    asm volatile("" ::: "memory");
+    if (g + NB - 1 < G) issue(g + NB - 1);  // into chunk g - 1's slot
+    const uint32_t rb = rd0 + (uint32_t)((g % NB) * CHUNK);
+#pragma unroll
+    for (int j = 0; j < KC / 4; j++) {
+      const f32x4 cv = *(const LDS_AS f32x4 *)(size_t)(rb + (uint32_t)(16 * (j ^ swz)));
+      const int j4 = g * (KC / 4) + j;
+#pragma unroll
+      for (int r = 0; r < RQ; r++) {
+        const f32x4 q4 = *(const f32x4 *)(qs + r * dp + 4 * j4);  // broadcast
+        acc[r] = fmaf(q4[0], cv[0], acc[r]);
+        acc[r] = fmaf(q4[1], cv[1], acc[r]);
+        acc[r] = fmaf(q4[2], cv[2], acc[r]);
+        acc[r] = fmaf(q4[3], cv[3], acc[r]);
+      }
+      if (XFORM && 4 * j4 < d8) {
+        // ndarray order: accumulator j sums x[8t + j]^2 over t
+        const int o = (j & 1) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; e++) p[o + e] = p[o + e] + cv[e] * cv[e];
+      }
+    }
+  }
+  float cnv = 0.0f;
+  if (XFORM && col < ns) {
+    float sum = 0.0f;
+    sum = sum + (p[0] + p[4]);
+    sum = sum + (p[1] + p[5]);
+    sum = sum + (p[2] + p[6]);
+    sum = sum + (p[3] + p[7]);
+    const float *crow = a.c + (int64_t)col * a.ldc;
+    for (int i = d8; i < d; i++) {
+      const float x = crow[i];
+      sum = sum + x * x;
+    }
+    cnv = a.squared ? sum : sqrt_rn<float>(sum);
+  }
+#pragma unroll
+  for (int r = 0; r < RQ; r++) {
+    u64 key = 0ull;
+    if (col < ns && row0 + r < m) {
+      const float sc = exact_score<METRIC>(acc[r], XFORM ? qn_s[r] : 0.0f, cnv);
+      key = ((u64)okey32(METRIC == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~(uint32_t)col);
+    }
+    keys[r * 256 + col] = key;
+  }
+  __syncthreads();
+  if (XFORM && tid < RQ && row0 + tid < m) a.qn[row0 + tid] = qn_s[tid];
+  const int row = row0 + w;
+  if (row >= m) return;
+  u64 x[4];
+#pragma unroll
+  for (int e = 0; e < 4; e++) x[e] = keys[w * 256 + lane + 64 * e];
+  const u64 th = wave_kth_u64<4>(x, a.k);  // nonzero: ns >= k keys, none of them 0
+  if (lane == 0) a.gthr[row] = th ? th - 1 : 0ull;
+}
+
+template <int E, int METRIC, int LDSK>
 __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   using namespace seedk;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   unsigned b = blockIdx.x;
+  if (LDSK) {
+    // every block: a slice of the zero fill (stores only, issued first), the
+    // seed (blocks < sblocks: one per 4 query rows), then a slice of the
+    // corpus norms (cper rows)
+    {
+      const int64_t tot = a.z0n + a.z1n, per = (tot + gridDim.x - 1) / gridDim.x;
+      const int64_t lo = (int64_t)b * per, hi = lo + per < tot ? lo + per : tot;
+      for (int64_t i = lo + tid; i < hi; i += 256) {
+        if (i < a.z0n) a.z0[i] = make_uint4(0u, 0u, 0u, 0u);
+        else a.z1[i - a.z0n] = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+    if (b < a.sblocks) seed_lds_block<METRIC>(a, b, smem);
+    if (a.cblocks) {
+      const int64_t lo = (int64_t)b * a.cper;
+      const int64_t rows = lo + a.cper < a.n ? a.cper : a.n - lo;
+      for (int64_t g0 = 0; g0 < rows * 8; g0 += 256)
+        norms_rows<float, float>(a.c + lo * a.ldc, rows, a.d, a.ldc, a.squared, a.cn + lo, a.cinv + lo, g0 + tid);
+    }
+    return;
+  }
   if (b >= a.sblocks) {
     b -= a.sblocks;
     if (b < a.qblocks) {
@@ -1067,12 +1147,6 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
       if (i < a.z0n) a.z0[i] = make_uint4(0u, 0u, 0u, 0u);
       else a.z1[i - a.z0n] = make_uint4(0u, 0u, 0u, 0u);
     }
-    return;
-  }
-  if (MFMA) {
-    // (a template parameter, not a branch: the fmaf-chain seed's registers
-    // would otherwise set this path's occupancy too)
-    seed_mfma_block<E, METRIC>(a, b, smem);
     return;
   }
   constexpr bool XFORM = METRIC != kMetricDot;
@@ -1170,34 +1244,36 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   if (lane == 0) a.gthr[row] = th ? th - 1 : 0ull;
 }
 
-template <int METRIC, int MFMA>
+template <int METRIC, int LDSK>
 static hipError_t launch_prologue_t2(const PrologueArgs &a, unsigned grid, hipStream_t s) {
   using namespace seedk;
   const size_t lds_base = (size_t)RQ * a.dp * 4 + RQ * 4;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute((const void *)prologue_kernel<4, METRIC, MFMA>,
+    hipError_t e = hipFuncSetAttribute((const void *)prologue_kernel<4, METRIC, LDSK>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void *)prologue_kernel<8, METRIC, MFMA>,
+    if (e == hipSuccess && !LDSK)
+      e = hipFuncSetAttribute((const void *)prologue_kernel<8, METRIC, LDSK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void *)prologue_kernel<16, METRIC, MFMA>,
+    if (e == hipSuccess && !LDSK)
+      e = hipFuncSetAttribute((const void *)prologue_kernel<16, METRIC, LDSK>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  // (MFMA seed blocks: 32 rows' keys + norms in LDS)
-  auto lds = [&](int nsp) { return MFMA ? (size_t)32 * nsp * 8 + 4 * (32 + nsp) : lds_base + RQ * nsp * 8; };
-  if (a.ns <= 256) prologue_kernel<4, METRIC, MFMA><<<grid, 256, lds(256), s>>>(a);
-  else if (a.ns <= 512) prologue_kernel<8, METRIC, MFMA><<<grid, 256, lds(512), s>>>(a);
-  else if (!MFMA) prologue_kernel<16, METRIC, MFMA><<<grid, 256, lds(1024), s>>>(a);
-  else return hipErrorInvalidValue;
+  if (LDSK) {  // (ns <= 256, dp <= kLdsMaxDp: checked by the caller)
+    prologue_kernel<4, METRIC, LDSK><<<grid, 256, (size_t)NB * CHUNK + RQ * 256 * 8 + lds_base, s>>>(a);
+    return hipGetLastError();
+  }
+  auto lds = [&](int nsp) { return lds_base + RQ * nsp * 8; };
+  if (a.ns <= 256) prologue_kernel<4, METRIC, LDSK><<<grid, 256, lds(256), s>>>(a);
+  else if (a.ns <= 512) prologue_kernel<8, METRIC, LDSK><<<grid, 256, lds(512), s>>>(a);
+  else prologue_kernel<16, METRIC, LDSK><<<grid, 256, lds(1024), s>>>(a);
   return hipGetLastError();
 }
 template <int METRIC>
 static hipError_t launch_prologue_t(const PrologueArgs &a, unsigned grid, hipStream_t s) {
-  return a.mfma_seed ? launch_prologue_t2<METRIC, 1>(a, grid, s) : launch_prologue_t2<METRIC, 0>(a, grid, s);
+  return a.lds_seed ? launch_prologue_t2<METRIC, 1>(a, grid, s) : launch_prologue_t2<METRIC, 0>(a, grid, s);
 }
 
 hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int64_t n,
@@ -1231,18 +1307,27 @@ hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const floa
   a.z1 = (uint4 *)z1;
   a.z0n = (int64_t)(z0_bytes / 16);
   a.z1n = (int64_t)(z1_bytes / 16);
-  // MFMA seed blocks (seed_mfma_block) only on request (PMM_SEED_MFMA=1, read
-  // per call) and when the sample's keys fit LDS: 32 blocks of 4 waves at c1
-  // walk their tiles one after another, latency-bound -- prologue 79 us
-  // against the fmaf-chain seed's 21 (c2: 43 vs 17; gpurun_out r4c, same box)
-  const char *sme = getenv("PMM_SEED_MFMA");
-  a.mfma_seed = (ns % 32 == 0 && ns <= 512 && sme && atoi(sme) == 1) ? 1 : 0;
-  a.sblocks = a.mfma_seed ? (unsigned)((m + 31) / 32) : (unsigned)((m + seedk::RQ - 1) / seedk::RQ);
+  // LDS-staged seed blocks (seed_lds_block) where they apply; PMM_SEED_LDS=0
+  // (read per call) keeps the fmaf-chain blocks that stream their own rows
+  const char *le = getenv("PMM_SEED_LDS");
+  a.lds_seed = (ns <= 256 && dp <= seedk::kLdsMaxDp && !(le && atoi(le) == 0)) ? 1 : 0;
+  a.sblocks = (unsigned)((m + seedk::RQ - 1) / seedk::RQ);
   const bool xf = metric != kMetricDot;
-  a.qblocks = xf ? (unsigned)((m * 8 + 255) / 256) : 0u;
-  a.cblocks = (xf && corpus_norms) ? (unsigned)((n * 8 + 255) / 256) : 0u;
-  a.zblocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((a.z0n + a.z1n + 255) / 256, 64));
-  const unsigned grid = a.sblocks + a.qblocks + a.cblocks + a.zblocks;
+  unsigned grid;
+  if (a.lds_seed) {
+    // one block kind: seed blocks, plus norms-only blocks so that no block
+    // takes more than 64 corpus norm rows
+    a.qblocks = 0u;
+    grid = std::max<unsigned>(a.sblocks, (xf && corpus_norms) ? (unsigned)((n + 63) / 64) : 1u);
+    a.cper = (n + grid - 1) / grid;
+    a.cblocks = (xf && corpus_norms) ? 1u : 0u;  // (a flag here)
+    a.zblocks = 0u;
+  } else {
+    a.qblocks = xf ? (unsigned)((m * 8 + 255) / 256) : 0u;
+    a.cblocks = (xf && corpus_norms) ? (unsigned)((n * 8 + 255) / 256) : 0u;
+    a.zblocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((a.z0n + a.z1n + 255) / 256, 64));
+    grid = a.sblocks + a.qblocks + a.cblocks + a.zblocks;
+  }
   if (metric == kMetricCosine) return launch_prologue_t<kMetricCosine>(a, grid, s);
   if (metric == kMetricDot) return launch_prologue_t<kMetricDot>(a, grid, s);
   return launch_prologue_t<kMetricEuclidean>(a, grid, s);

@@ -23,7 +23,8 @@ BUILDS = [("pmm_bf16_ws_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] 
     ("pmm_bf16_ks.hip", ("-DPMM_BF16_KS=6",)),
 ] + [
     ("pmm_bf16_r64_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
-    ("pmm_bf16_ff_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)]
+    ("pmm_bf16_ff_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
+    ("pmm_kernels.hip", ())]  # (the f32 seed prologue's asm LDS-DMA)
 
 
 def have_hipcc():

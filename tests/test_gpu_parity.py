@@ -922,9 +922,9 @@ def test_threshold_seeding_changes_nothing(pmm, k, d, monkeypatch):
         monkeypatch.setenv("PMM_SEED_GEMM", "1")
         got_g = gpu_topk(q, c, k, metric)
         monkeypatch.delenv("PMM_SEED_GEMM")
-        monkeypatch.setenv("PMM_SEED_MFMA", "1")  # the MFMA seed blocks (opt-in)
+        monkeypatch.setenv("PMM_SEED_LDS", "0")  # the seed blocks that stream their own rows
         got_f = gpu_topk(q, c, k, metric)
-        monkeypatch.delenv("PMM_SEED_MFMA")
+        monkeypatch.delenv("PMM_SEED_LDS")
         monkeypatch.delenv("PMM_SEED")
         for g in (got, got_g, got_f):
             assert np.array_equal(g[0], want[0]), metric
@@ -934,15 +934,15 @@ def test_threshold_seeding_changes_nothing(pmm, k, d, monkeypatch):
 
 
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-@pytest.mark.parametrize("seed_mfma", ["1", "0"])
+@pytest.mark.parametrize("seed_lds", ["1", "0"])
 @pytest.mark.parametrize("d", [256, 96, 37])
-def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, seed_mfma, d, monkeypatch):
+def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, seed_lds, d, monkeypatch):
     # Every row's true top-k lies inside the seed sample (the corpus's first
     # ns = 256 rows hold 16 near-copies of each query).  The seed's threshold
     # is (the sample's k-th composite) - 1, so if the seed scored the k-th
     # element even one ulp above the main pass, the main pass would reject
     # that element and the list would lose it: bit-exactness against the
-    # oracle here checks that the seed (MFMA blocks or fmaf chains) computes
+    # oracle here checks that the seed (LDS-staged or row-streaming blocks) computes
     # the main pass's scores bit for bit
     rs = np.random.RandomState(17 + METRICS[metric] + d)
     m, N, k = 16, 4096, 10
@@ -950,11 +950,11 @@ def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, see
     c = (rs.randn(N, d) * 0.3).astype(np.float32)
     c[:256] = q[np.arange(256) % m] + 0.05 * rs.randn(256, d).astype(np.float32)
     monkeypatch.setenv("PMM_SEED", "1")
-    monkeypatch.setenv("PMM_SEED_MFMA", seed_mfma)
+    monkeypatch.setenv("PMM_SEED_LDS", seed_lds)
     idx, sc = gpu_topk(q, c, k, metric)
     assert int(idx.max()) < 256  # the top-k really is inside the sample
     oi, osc = oracle.topk(q, c, k, METRICS[metric])
-    assert_bitexact(idx, sc, oi, osc, f"seed-sample top-k {metric} mfma={seed_mfma}")
+    assert_bitexact(idx, sc, oi, osc, f"seed-sample top-k {metric} lds={seed_lds}")
 
 
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
