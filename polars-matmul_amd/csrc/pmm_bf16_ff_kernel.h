@@ -268,6 +268,7 @@ __global__ __launch_bounds__(ff::NTH, 1) void gemm_bf16_ff_kernel(GemmF32Args a)
       lo_base = (uint32_t)(size_t)(LDS_AS float *)(lo_w + 4 * gp);
     };
     auto pre = [&](const AccSet &P, int e) __attribute__((always_inline)) {
+      if (PMM_ABL(a.ablate & 1)) return;  // (lab: no pre-filter at all)
       const int b = e >> 3, cb = (e >> 2) & 1, i = e & 3;
       if ((e & 7) == 0) lo4 = *(const LDS_AS f32x4 *)(size_t)(lo_base + 64u * (uint32_t)b);
       const float v = P[b][cb][i];
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(ff::NTH, 1) void gemm_bf16_ff_kernel(GemmF32Args a)
       // count stays in an SGPR; past the region's capacity nothing is stored
       // but the count runs on (the bucket pass then re-runs the region's rows)
       const unsigned slot = nreg + (unsigned)lanes_below(mk);
-      const bool put = pass && slot < (unsigned)a.ffcap;
+      const bool put = pass && slot < (unsigned)a.ffcap && !PMM_ABL(a.ablate & 2);  // (lab: no stores)
       if (put) {
         const uint32_t hi = (cb ? hib1 : hib0) + ((uint32_t)(16 * b + i) << 26);
         reg[slot] = ((u64)hi << 32) | (u64)__float_as_uint(v);

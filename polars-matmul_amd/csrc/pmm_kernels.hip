@@ -1307,10 +1307,13 @@ hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const floa
   a.z1 = (uint4 *)z1;
   a.z0n = (int64_t)(z0_bytes / 16);
   a.z1n = (int64_t)(z1_bytes / 16);
-  // LDS-staged seed blocks (seed_lds_block) where they apply; PMM_SEED_LDS=0
-  // (read per call) keeps the fmaf-chain blocks that stream their own rows
+  // The fmaf-chain blocks that stream their own rows by default; PMM_SEED_LDS=1
+  // (read per call) takes the LDS-staged seed blocks (seed_lds_block) where
+  // they apply.  A/B on one box, two alternations (profiles/r4_seed/): c1 step
+  // 0.104 ms with the LDS-staged blocks against 0.099 ms (prologue 24 vs
+  // 20 us), c2 0.096 vs 0.095 ms; bit-identical either way.
   const char *le = getenv("PMM_SEED_LDS");
-  a.lds_seed = (ns <= 256 && dp <= seedk::kLdsMaxDp && !(le && atoi(le) == 0)) ? 1 : 0;
+  a.lds_seed = (ns <= 256 && dp <= seedk::kLdsMaxDp && le && atoi(le) == 1) ? 1 : 0;
   a.sblocks = (unsigned)((m + seedk::RQ - 1) / seedk::RQ);
   const bool xf = metric != kMetricDot;
   unsigned grid;

@@ -922,7 +922,7 @@ def test_threshold_seeding_changes_nothing(pmm, k, d, monkeypatch):
         monkeypatch.setenv("PMM_SEED_GEMM", "1")
         got_g = gpu_topk(q, c, k, metric)
         monkeypatch.delenv("PMM_SEED_GEMM")
-        monkeypatch.setenv("PMM_SEED_LDS", "0")  # the seed blocks that stream their own rows
+        monkeypatch.setenv("PMM_SEED_LDS", "1")  # the LDS-staged seed blocks (opt-in)
         got_f = gpu_topk(q, c, k, metric)
         monkeypatch.delenv("PMM_SEED_LDS")
         monkeypatch.delenv("PMM_SEED")
