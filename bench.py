@@ -804,21 +804,34 @@ def cpu_selftest(args, rank, world):
 F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X FP64 matrix, AMD spec (MI355X_MICROARCH.md lists no f64 row)
 
 
-def f64_line(steps=200, warmup=10):
+F64_LARGE = (4096, 1_000_000, 256, 10, "cosine")  # the f64 path where the M x N matrix (32 GB) must not exist
+
+
+def f64_line(steps=200, warmup=10, large=False):
     """the f64 top-k (what Polars' default Float64 columns
-    take; src/matmul.rs:449-468) at the reference benchmark's size, c1 inputs
-    as f64 (seed 42, cosine, k = 10), resident in HBM: pmm_topk_f64_device per
-    step, fused (default) and materialised (PMM_F64_FUSED=0) alternately timed;
-    the GEMM launches' roofline against the f64 MFMA peak."""
+    take; src/matmul.rs:449-468) resident in HBM: pmm_topk_f64_device per
+    step, fused (PMM_F64_FUSED=1) and materialised (PMM_F64_FUSED=0) timed one
+    after the other, plus the library's default choice; the GEMM launches'
+    roofline against the f64 MFMA peak.  large=False: the reference
+    benchmark's size, c1 inputs as f64 (seed 42, cosine, k = 10);
+    large=True: F64_LARGE, device-generated N(0,1) rows (seed 7)."""
     import torch
     from polars_matmul import _native
 
-    M, N, D, k, metric = CONFIGS["c1"][:5]
-    mid = _native.metric_from_str(metric)
-    qh, ch = ref_inputs(M, N, D)
     dev = torch.device("cuda", torch.cuda.current_device())
-    q = torch.from_numpy(qh.astype(np.float64)).to(dev)
-    c = torch.from_numpy(ch.astype(np.float64)).to(dev)
+    if large:
+        M, N, D, k, metric = F64_LARGE
+        g = torch.Generator(device=dev)
+        g.manual_seed(7)
+        q = torch.randn((M, D), dtype=torch.float64, device=dev, generator=g)
+        c = torch.randn((N, D), dtype=torch.float64, device=dev, generator=g)
+        qh, ch = None, None
+    else:
+        M, N, D, k, metric = CONFIGS["c1"][:5]
+        qh, ch = ref_inputs(M, N, D)
+        q = torch.from_numpy(qh.astype(np.float64)).to(dev)
+        c = torch.from_numpy(ch.astype(np.float64)).to(dev)
+    mid = _native.metric_from_str(metric)
     oi = torch.empty((M, k), dtype=torch.int32, device=dev)
     os_ = torch.empty((M, k), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
@@ -827,10 +840,11 @@ def f64_line(steps=200, warmup=10):
         _native.topk_f64_device(q.data_ptr(), D, M, c.data_ptr(), D, N, D, k, mid, oi.data_ptr(), os_.data_ptr(),
                                 stream=stream)
 
-    out = {"workload": f"{M}x{N}x{D} f64 {metric} k={k} (c1 inputs as f64)", "dtype": "f64"}
-    for mode in ("fused", "materialised"):
-        if mode == "materialised":
-            os.environ["PMM_F64_FUSED"] = "0"
+    out = {"workload": f"{M}x{N}x{D} f64 {metric} k={k} " +
+           ("(device N(0,1) rows)" if large else "(c1 inputs as f64)"), "dtype": "f64"}
+    for mode in ("fused", "materialised", "default"):
+        if mode != "default":
+            os.environ["PMM_F64_FUSED"] = "1" if mode == "fused" else "0"
         try:
             for _ in range(warmup):
                 run()
@@ -845,8 +859,9 @@ def f64_line(steps=200, warmup=10):
             _native.timing_enable(False)
         finally:
             os.environ.pop("PMM_F64_FUSED", None)
-        gname = "gemm_f64_topk" if mode == "fused" else "gemm_f64_scores"
-        gms, gn = _native.timing_read(gname)
+        gms, gn = _native.timing_read("gemm_f64_topk")
+        if not gn:
+            gms, gn = _native.timing_read("gemm_f64_scores")
         tot, tn = _native.timing_read("")
         ach = 2.0 * M * N * D / (gms / steps / 1000.0) / 1e12 if gn else None
         rec = {"value": round(M * steps / el, 2), "unit": "queries/s", "ms_per_step": round(el / steps * 1000.0, 4),
@@ -859,12 +874,15 @@ def f64_line(steps=200, warmup=10):
                                "peak_source": "AMD spec (FP64 matrix); not in MI355X_MICROARCH.md"}
         out[mode] = rec
         log(f"f64 {mode}: {rec}")
-    # exactness of this run's lists against the oracle (first 64 rows)
+    # exactness of this run's lists against the oracle (first rows)
     import oracle
 
+    nr = 4 if large else 64
     got = oi.cpu().numpy().view(np.uint32)
-    oi_, _ = oracle.topk(qh[:64].astype(np.float64), ch.astype(np.float64), k, oracle.metric_from_str(metric))
-    out["check"] = {"rows": 64, "exact_index_match_frac": float(np.mean(got[:64] == oi_))}
+    if large:
+        qh, ch = q[:nr].cpu().numpy(), c.cpu().numpy()
+    oi_, _ = oracle.topk(qh[:nr].astype(np.float64), ch.astype(np.float64), k, oracle.metric_from_str(metric))
+    out["check"] = {"rows": nr, "exact_index_match_frac": float(np.mean(got[:nr] == oi_))}
     del q, c
     torch.cuda.empty_cache()
     return out
@@ -1065,7 +1083,8 @@ def main():
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
     ap.add_argument("--extra", default="c4,c1,c2,c1_f64,matmul",
                     help="comma-separated secondary configs measured after the main line (N=1; 'none' = none; "
-                         "'matmul' = .pmm.matmul at the c1 size; 'c1_f64' = the f64 top-k at the c1 size)")
+                         "'matmul' = .pmm.matmul at the c1 size; 'c1_f64' = the f64 top-k at the c1 size; "
+                         "'f64_large' = the f64 top-k at 4096 x 1M x 256)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 top-k")
     ap.add_argument("--timing-stride", type=int, default=0,
                     help="record the per-kernel HIP events on every n-th timed step (0: every step of "
@@ -1170,6 +1189,7 @@ def main():
         extra = {}
         for name in [x for x in args.extra.split(",") if x and x not in (args.config, "none")]:
             extra[name] = (matmul_line(args) if name == "matmul" else f64_line() if name == "c1_f64"
+                           else f64_line(steps=3, warmup=1, large=True) if name == "f64_large"
                            else extra_line(name, args.steps, args.warmup, dev, args))
             log(f"extra {name}: {json.dumps(extra[name])}")
 

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -1434,9 +1435,19 @@ size_t f64_workspace_bytes(int64_t m, int64_t n, int64_t k, int metric) {
   return std::max(p.total, mp.total);
 }
 
-bool f64_fused_enabled() {
-  const char *e = getenv("PMM_F64_FUSED");  // read per call (tests compare both paths)
-  return !(e && atoi(e) == 0);
+// Fused scan or materialised scores, by the size of the M x N f64 score
+// matrix the materialised path writes and re-reads: at the reference
+// benchmark's size (1000 x 10000, 80 MB) the materialised path's one store
+// GEMM + row select measured 0.232 ms per call against 0.318 for the fused
+// scan's two chunk launches, two selects and its overflow check
+// (profiles/r4_f64/); the fused scan is for matrices that would not fit or
+// would cost their HBM round trip.  PMM_F64_FUSED=1 / 0 forces either
+// (read per call: tests compare both paths).
+constexpr double kF64FusedMinMatrixBytes = 1024.0 * 1024.0 * 1024.0;
+bool f64_fused_enabled(int64_t m, int64_t n) {
+  const char *e = getenv("PMM_F64_FUSED");
+  if (e && *e) return atoi(e) != 0;
+  return (double)m * (double)n * 8.0 > kF64FusedMinMatrixBytes;
 }
 
 int topk_f64_materialised(const double *dq, int64_t ldq, int64_t m, const double *dc, int64_t ldc, int64_t n,
@@ -1485,7 +1496,7 @@ int topk_f64_materialised(const double *dq, int64_t ldq, int64_t m, const double
 int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double *dc, int64_t ldc, int64_t n,
                          int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *oi, double *os, char *w,
                          hipStream_t s) {
-  if (k > kFusedMaxK || !f64_fused_enabled())
+  if (k > kFusedMaxK || !f64_fused_enabled(m, n))
     return topk_f64_materialised(dq, ldq, m, dc, ldc, n, d, k, metric, index_base, oi, os, w, s);
   F64Plan p;
   plan_f64(m, n, k, p);
@@ -1499,9 +1510,20 @@ int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double 
     HIP_TRY(launch_norms_f64(dc, n, d, ldc, sq, cn, s));
   }
   // chunk schedule: the first chunk fills half a buffer (accept-all), later
-  // chunks are g times the columns seen, about g*k survivors per row each
+  // chunks are g times the columns seen.  After `seen` columns the threshold
+  // is the k-th best of them, so a chunk of g * seen columns from the same
+  // distribution leaves ~g * X survivors in a row, X ~ Gamma(k) (the k-th
+  // order statistic's quantile times seen).  Its spread is k^-1/2 of its mean
+  // whatever `seen` is, so g is sized for the tail, not the mean: with
+  // P(X > k + t) <= exp(-t^2 / (2 (k + t))) and t = 23 + sqrt(529 + 46 k)
+  // (a per-row, per-chunk tail of e^-23 ~ 1e-10), g (k + t) <= cap - k keeps
+  // every row inside its buffer.  (g = (cap/2 - k) / k, sized for the mean,
+  // overflowed some row of nearly every call at 4096 x 1M: the whole call
+  // then re-ran materialised, 257 vs 209 ms; profiles/r4_f64/.)  Adversarial
+  // orders still overflow and fall back below.
   const int64_t s0 = std::min<int64_t>(n, p.cap / 2);
-  const int64_t g = std::max<int64_t>(1, (p.cap / 2 - k) / std::max<int64_t>(k, 1));
+  const double tail = 23.0 + std::sqrt(529.0 + 46.0 * (double)k);
+  const int64_t g = std::max<int64_t>(1, (int64_t)((double)(p.cap - k) / ((double)k + tail)));
   HIP_TRY(hipMemsetAsync(flag, 0, 4, s));
   for (int64_t r0 = 0; r0 < m; r0 += p.mc) {
     const int rows = (int)std::min<int64_t>(p.mc, m - r0);

@@ -188,6 +188,7 @@ def test_f64_fused_vs_oracle_and_materialised(pmm, m, n, d, k, metric, monkeypat
     c[n - 30:] = c[:30]  # exact ties across chunk boundaries
     c[n // 2] = 0.0      # a zero-norm corpus row
     q[0] = c[5]          # a query equal to a corpus row
+    monkeypatch.setenv("PMM_F64_FUSED", "1")  # (by size these shapes take the materialised path)
     idx, sc = gpu_topk(q, c, k, metric)
     assert sc.dtype == np.float64 and idx.shape == (m, min(k, n))
     oi, osc = oracle.topk(q, c, k, METRICS[metric])
@@ -201,10 +202,13 @@ def test_f64_fused_vs_oracle_and_materialised(pmm, m, n, d, k, metric, monkeypat
     assert np.array_equal(ms.view(np.uint64), sc.view(np.uint64))
 
 
-def test_f64_fused_scores_bitwise_vs_oracle(pmm):
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_f64_fused_scores_bitwise_vs_oracle(pmm, fused, monkeypatch):
     # v_mfma_f64_16x16x4_f64 fed K in natural order (lane kq holds k0 + 4s + kq
     # at step s): if the instruction accumulates its four products as a
-    # k-ordered fma chain, every score equals the oracle's bit for bit
+    # k-ordered fma chain, every score equals the oracle's bit for bit (fused
+    # scan and materialised scores alike)
+    monkeypatch.setenv("PMM_F64_FUSED", fused)
     rs = np.random.RandomState(77)
     q, c = rs.randn(40, 256), rs.randn(5000, 256)
     for metric in ("dot", "cosine", "euclidean"):
@@ -214,10 +218,11 @@ def test_f64_fused_scores_bitwise_vs_oracle(pmm):
         assert np.array_equal(sc.view(np.uint64), osc.view(np.uint64)), metric
 
 
-def test_f64_fused_overflow_falls_back(pmm):
+def test_f64_fused_overflow_falls_back(pmm, monkeypatch):
     # adversarial order: every corpus row beats every earlier one, so each
     # chunk's survivors overflow the buffers; the call must still be exact
     # (materialised fallback)
+    monkeypatch.setenv("PMM_F64_FUSED", "1")
     n, d = 20000, 16
     q = np.ones((4, d))
     c = np.repeat(np.arange(n, dtype=np.float64)[:, None], d, axis=1) / n
@@ -227,7 +232,9 @@ def test_f64_fused_overflow_falls_back(pmm):
     assert np.array_equal(idx, oi) and np.array_equal(sc, osc)
 
 
-def test_f64_nan_rows_and_k_equals_n(pmm):
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_f64_nan_rows_and_k_equals_n(pmm, fused, monkeypatch):
+    monkeypatch.setenv("PMM_F64_FUSED", fused)
     rs = np.random.RandomState(5)
     q, c = rs.randn(9, 24), rs.randn(1500, 24)
     c[[3, 700, 1499]] = np.nan
@@ -237,6 +244,30 @@ def test_f64_nan_rows_and_k_equals_n(pmm):
             oi, osc = oracle.topk(q, c, k, METRICS[metric])
             assert exact_match_rate(idx, oi) == 1.0, (metric, k)
             np.testing.assert_allclose(sc, osc, rtol=1e-12, atol=1e-12, equal_nan=True)
+
+
+@pytest.mark.parametrize("k", [1, 10, 100])
+def test_f64_fused_long_corpus_stays_fused(pmm, k, monkeypatch):
+    # Random rows over a long corpus: the chunk schedule is sized for the
+    # tail of the per-row survivor count (pmm_capi.hip, topk_f64_device_impl),
+    # so no row's buffer overflows and the call never falls back to the
+    # materialised path (whose score launches would show in the timers).
+    # With the growth sized for the mean, k = 1 overflowed ~13% of the rows.
+    n = _native()
+    rs = np.random.RandomState(900 + k)
+    q, c = rs.randn(256, 32), rs.randn(300_000, 32)
+    monkeypatch.setenv("PMM_F64_FUSED", "1")
+    n.timing_reset()
+    n.timing_enable(True)
+    try:
+        idx, sc = gpu_topk(q, c, k, "cosine")
+    finally:
+        n.timing_enable(False)
+    assert n.timing_read("gemm_f64_topk")[1] >= 2
+    assert n.timing_read("gemm_f64_scores")[1] == 0, "the fused scan overflowed and fell back"
+    oi, osc = oracle.topk(q[:16], c, k, METRICS["cosine"])
+    assert np.array_equal(idx[:16], oi)
+    assert np.array_equal(sc[:16].view(np.uint64), osc.view(np.uint64))
 
 
 def test_f64_device_api_equals_host(pmm):
