@@ -114,6 +114,9 @@ constexpr int drain_tiles() { return KS == 1 ? (PMM_WS_DRAIN_TILES < 2 ? PMM_WS_
 #ifndef PMM_WS_NST
 #define PMM_WS_NST 7  // (A/B override: -DPMM_WS_NST=n)
 #endif
+#ifndef PMM_WS_MFMA16
+#define PMM_WS_MFMA16 0  // 1: the MFMA waves (and the seed) on v_mfma_f32_16x16x32_bf16
+#endif
 template <int KS>
 struct Carve {
   static constexpr int NHB = KS >= 3 ? 1 : 2;              // hand-off buffers
@@ -189,6 +192,23 @@ __device__ __forceinline__ void mfma_drain(f32x16 (&acc)[NB]) {
   asm volatile("s_nop 7\n\ts_nop 4" : "+v"(acc[0]), "+v"(acc[NB - 1]));
 #pragma unroll
   for (int c = 1; c < NB - 1; c++) asm volatile("" : "+v"(acc[c]));
+}
+// The 16x16x32 form (PMM_WS_MFMA16): the MFMA waves' 32 x 64 block as 2 x 4
+// accumulators of 16 x 16, each K step of 32 in natural order (lane group g
+// of 16 lanes carries k 8g .. 8g + 7).  Same cycles per flop as 32x32x16 on
+// one SIMD; MI355X_MICROARCH.md measured bare loops of this shape at ~1.15x
+// the FLOP/s of the 32x32x16 form on random data (the chip holds a higher
+// clock on it).
+__device__ __forceinline__ void mfma16_acc(f32x4 &c, const bf16x8 &a, const bf16x8 &b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b) : "memory");
+}
+__device__ __forceinline__ void mfma16_first(f32x4 &c, const bf16x8 &a, const bf16x8 &b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=&v"(c) : "v"(a), "v"(b) : "memory");
+}
+__device__ __forceinline__ void mfma16_drain(f32x4 (&acc)[2][2 * NB]) {
+  asm volatile("s_nop 7\n\ts_nop 4" : "+v"(acc[0][0]), "+v"(acc[1][2 * NB - 1]));
+#pragma unroll
+  for (int i = 1; i < 4 * NB - 1; i++) asm volatile("" : "+v"(acc[i / (2 * NB)][i % (2 * NB)]));
 }
 }  // namespace ws
 
@@ -307,6 +327,21 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
         // the descriptor may be fresh from a VALU write (readfirstlane):
         // 5 wait states before a VMEM instruction reads it (hipcc pads
         // nothing in front of an asm statement)
+#if PMM_WS_MFMA16
+        // fragment i = 8 ks + 2 j + rb: rows 16 rb + (lane & 15), k 128 ks +
+        // 32 j + 8 (lane >> 4) .. + 7 (the row block in the scalar offset,
+        // which gets the same 5 wait states as the descriptor)
+        const uint32_t qoff16 = (uint32_t)((lane & 15) * a.ldq * 2 + 16 * (lane >> 4));
+        const uint32_t rbo = __builtin_amdgcn_readfirstlane((uint32_t)(16 * a.ldq * 2));
+        asm volatile("s_nop 4" ::"s"(rq), "s"(rbo));
+#pragma unroll
+        for (int i = 0; i < KSUB * KS; i++)
+          asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen offset:%4"
+                       : "=v"(af[i])
+                       : "v"(qoff16), "s"(rq), "s"((i & 1) ? rbo : 0u), "i"(((i / KSUB) * 128 + ((i % KSUB) / 2) * 32) * 2)
+                       : "memory");
+        (void)qoff;
+#else
         asm volatile("s_nop 4" ::"s"(rq));
 #pragma unroll
         for (int i = 0; i < KSUB * KS; i++)
@@ -314,6 +349,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
                        : "=v"(af[i])
                        : "v"(qoff), "s"(rq), "i"(((i / KSUB) * 128 + (i % KSUB) * 8) * 2)
                        : "memory");
+#endif
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       // LDS byte address of this lane's fragment chunk: column r32 of a group
@@ -321,12 +357,26 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       // since 8h + sub = 8h ^ sub (sub < 8), substep sub's address is the
       // sub-0 address XOR (sub << 4): one v_xor per substep, no per-substep
       // address registers (the A rows leave ~60 VGPRs for everything else)
+#if PMM_WS_MFMA16
+      // 16x16x32 form: substep sub = half-step (j = sub / 2: k 32 j .. 32 j +
+      // 31 of the K-step; half = sub % 2: column blocks 2 half, 2 half + 1);
+      // lane (c16, g) reads chunk 4 j + g of column 16 cb + c16, stored at
+      // chunk (4 j + g) ^ c16 = (g ^ c16) ^ 4 j: the lane's sub-0 address
+      // XOR (j << 6), plus 16 cb columns
+      const int c16 = lane & 15, g4 = lane >> 4;
+      const uint32_t lane_off = (uint32_t)(c16 * KB + 16 * (g4 ^ c16));
+#else
       const uint32_t lane_off = (uint32_t)(r32 * KB + 16 * ((8 * h) ^ (r32 & 15)));
+#endif
       const uint32_t ring_lds = (uint32_t)(size_t)(LDS_AS char *)ring;
       int sl = 0;
       for (int tile = t0; tile < t1; tile++) {
         if constexpr (C::SLOT_REPEATS) asm volatile("" : "+s"(sl));  // (see Carve)
+#if PMM_WS_MFMA16
+        f32x4 acc[2][2 * NB];  // [row block][column block of 16]
+#else
         f32x16 acc[NB];
+#endif
         bf16x8 bq[PF + 1][NB];  // fragment sets: PF in flight + the one in use
 #pragma unroll
         for (int ks = 0; ks < KS; ks++) {
@@ -343,9 +393,15 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
 #ifdef PMM_WS_NOFRAG
             return;  // diagnostic build only: MFMAs on stale fragments, no LDS reads
 #endif
+#if PMM_WS_MFMA16
+            const uint32_t ad = (base ^ (uint32_t)((sub >> 1) << 6)) + (uint32_t)((sub & 1) * 2 * 16 * KB);
+#pragma unroll
+            for (int c = 0; c < NB; c++) bq[set][c] = *(const LDS_AS bf16x8 *)(size_t)(ad + c * 16 * KB);
+#else
             const uint32_t ad = base ^ (uint32_t)(sub << 4);
 #pragma unroll
             for (int c = 0; c < NB; c++) bq[set][c] = *(const LDS_AS bf16x8 *)(size_t)(ad + c * 32 * KB);
+#endif
           };
           // fragments stream PF substeps ahead across the K-steps of a tile:
           // step g + 1's slot landed before B_g, so its first PF substeps are
@@ -361,24 +417,55 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             const int gs = g0 + sub;
             if (sub + PF < KSUB) rd(sbase, sub + PF, (gs + PF) % (PF + 1));
             else if (ks < KS - 1) rd(nbase, sub + PF - KSUB, (gs + PF) % (PF + 1));
+#if PMM_WS_MFMA16
+            {
+              const int j = sub >> 1, half = sub & 1;
+#pragma unroll
+              for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+                for (int c = 0; c < NB; c++) {
+                  const bf16x8 &A = af[KSUB * ks + 2 * j + rb];
+                  if (ks == 0 && j == 0) mfma16_first(acc[rb][2 * half + c], A, bq[gs % (PF + 1)][c]);
+                  else mfma16_acc(acc[rb][2 * half + c], A, bq[gs % (PF + 1)][c]);
+                }
+            }
+#else
 #pragma unroll
             for (int c = 0; c < NB; c++) {
               if (gs == 0) mfma_first(acc[c], af[0], bq[0][c]);
               else mfma_acc(acc[c], af[gs], bq[gs % (PF + 1)][c]);
             }
+#endif
             __builtin_amdgcn_sched_barrier(0);
           }
           sl = sn;
         }
-        mfma_drain(acc);
         // hand the tile to the epilogue wave of these rows
         char *hb = smem + OFF_HAND + ((tile % NHB) * NWM + rw) * HAND;
+#if PMM_WS_MFMA16
+        mfma16_drain(acc);
+        // in the 32x32 accumulator layout the epilogue reads: the 4-row group
+        // 16 rb + 4 g of column 16 cb + c16 is f32x4 (column block cb / 2,
+        // q = 2 rb + g / 2) of lane 16 (cb % 2) + c16 + 32 (g % 2)
+        // (one lane address, the rest immediate offsets; kept opaque so hipcc
+        // does not hoist eight addresses out of the tile loop)
+        uint32_t hl = (uint32_t)(size_t)(LDS_AS char *)hb + (uint32_t)(((g4 >> 1) * 64 + c16 + 32 * (g4 & 1)) * 16);
+        asm volatile("" : "+v"(hl));
+#pragma unroll
+        for (int rb = 0; rb < 2; rb++)
+#pragma unroll
+          for (int cb = 0; cb < 2 * NB; cb++)
+            *(LDS_AS f32x4 *)(size_t)(hl + (uint32_t)((((cb >> 1) * 4 + 2 * rb) * 64 + 16 * (cb & 1)) * 16)) =
+                acc[rb][cb];
+#else
+        mfma_drain(acc);
 #pragma unroll
         for (int c = 0; c < NB; c++)
 #pragma unroll
           for (int q = 0; q < 4; q++)
             *(f32x4 *)(hb + ((c * 4 + q) * 64 + lane) * 16) =
                 (f32x4){acc[c][4 * q], acc[c][4 * q + 1], acc[c][4 * q + 2], acc[c][4 * q + 3]};
+#endif
       }
       // the epilogue waves' last tile: two more barriers
       wait_lgkm0();
@@ -732,19 +819,32 @@ __global__ __launch_bounds__(256, 1) void seed_bf16_ws_kernel(GemmF32Args a, flo
   if (active) {
     const __amdgpu_buffer_rsrc_t rq =
         make_rsrc(a.qb + (int64_t)wrow0 * a.ldq, (int64_t)min(32, a.M - wrow0) * a.ldq * 2);
-    const uint32_t qoff = (uint32_t)(r32 * a.ldq * 2 + 128 * h);
     // (compiler-visible loads: these registers may be moved before use, and
     // an asm load's destination must not be read before its wait)
+#if PMM_WS_MFMA16
+    const uint32_t qoff = (uint32_t)((lane & 15) * a.ldq * 2 + 16 * (lane >> 4));
+#pragma unroll
+    for (int i = 0; i < G; i++)
+      af[i] = __builtin_bit_cast(
+          bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                      rq, (int)(qoff + (i & 1) * 16 * a.ldq * 2 + ((i / KSUB) * 128 + ((i % KSUB) / 2) * 32) * 2), 0, 0));
+#else
+    const uint32_t qoff = (uint32_t)(r32 * a.ldq * 2 + 128 * h);
 #pragma unroll
     for (int i = 0; i < G; i++)
       af[i] = __builtin_bit_cast(
           bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rq, (int)(qoff + ((i / KSUB) * 128 + (i % KSUB) * 8) * 2), 0, 0));
+#endif
   }
   constexpr bool XFORM = METRIC != kMetricDot;
   float qv[16];
 #pragma unroll
   for (int e = 0; e < 16; e++) {
+#if PMM_WS_MFMA16
+    const int row = wrow0 + 16 * (e >> 2) + 4 * (lane >> 4) + (e & 3);  // e = 4 rb + i
+#else
     const int row = wrow0 + acc_row(e, h);
+#endif
     qv[e] = (XFORM && row < a.M) ? a.qn[row] : 0.0f;
   }
   const __amdgpu_buffer_rsrc_t rc = make_rsrc(a.cb, (int64_t)ns * a.ldc * 2);
@@ -774,6 +874,38 @@ __global__ __launch_bounds__(256, 1) void seed_bf16_ws_kernel(GemmF32Args a, flo
   __syncthreads();
   for (int t = 0; t < nt; t++) {
     if (t + 1 < nt) fetch(t + 1);
+#if PMM_WS_MFMA16
+    if (active) {
+      // lane (c16, g): column block cb of 16, K-step ks, step j: column
+      // t 32 + 16 cb + c16, k 128 ks + 32 j + 8 g .. + 7 -- the main pass's
+      // chain per 16 x 16 block, K in natural order
+      typedef __bf16 bf16v8 __attribute__((ext_vector_type(8)));
+      const int c16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+      for (int cb = 0; cb < 2; cb++) {
+        const int col = t * 32 + 16 * cb + c16;
+        const char *base = smem + (t & 1) * 32 * SC::RS + (16 * cb + c16) * SC::RS + 16 * g4;
+        f32x4 acc[2] = {{}, {}};
+#pragma unroll
+        for (int ks = 0; ks < KS; ks++)
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            const bf16x8 b = *(const bf16x8 *)(base + (ks * 128 + 32 * j) * 2);
+#pragma unroll
+            for (int rb = 0; rb < 2; rb++)
+              acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                  __builtin_bit_cast(bf16v8, af[KSUB * ks + 2 * j + rb]), __builtin_bit_cast(bf16v8, b), acc[rb], 0,
+                  0, 0);
+          }
+        const float cv = XFORM ? a.cn[col] : 0.0f;
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const int row = wrow0 + 16 * (e >> 2) + 4 * g4 + (e & 3);
+          if (row < a.M) S[(int64_t)row * ns + col] = exact_score<METRIC>(acc[e >> 2][e & 3], qv[e], cv);
+        }
+      }
+    }
+#else
     if (active) {
       const int col = t * 32 + r32;
       // lane (r32, h), substep gs: column col, K-step gs / 8, chunk 8h + gs % 8
@@ -796,6 +928,7 @@ __global__ __launch_bounds__(256, 1) void seed_bf16_ws_kernel(GemmF32Args a, flo
         if (row < a.M) S[(int64_t)row * ns + col] = exact_score<METRIC>(acc[e], qv[e], cv);
       }
     }
+#endif
     // block t + 1 into the buffer block t - 1 used (every wave left it at
     // the previous barrier); visible to all after this one
     if (t + 1 < nt) put((t + 1) & 1);

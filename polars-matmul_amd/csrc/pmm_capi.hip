@@ -1436,14 +1436,13 @@ size_t f64_workspace_bytes(int64_t m, int64_t n, int64_t k, int metric) {
 }
 
 // Fused scan or materialised scores, by the size of the M x N f64 score
-// matrix the materialised path writes and re-reads: at the reference
-// benchmark's size (1000 x 10000, 80 MB) the materialised path's one store
-// GEMM + row select measured 0.232 ms per call against 0.318 for the fused
-// scan's two chunk launches, two selects and its overflow check
-// (profiles/r4_f64/); the fused scan is for matrices that would not fit or
-// would cost their HBM round trip.  PMM_F64_FUSED=1 / 0 forces either
-// (read per call: tests compare both paths).
-constexpr double kF64FusedMinMatrixBytes = 1024.0 * 1024.0 * 1024.0;
+// matrix the materialised path writes and re-reads (device API, cosine,
+// k = 10, D = 256; profiles/r4_f64/f64_sizes.jsonl): 1000 x 10000 (80 MB)
+// materialised 0.239 ms vs fused 0.348 (its chunk launches, selects and
+// overflow check); 1000 x 100000 (0.8 GB) 2.02 vs 1.40; 4096 x 1M (33 GB)
+// 209 vs 47.6.  The threshold sits between the first two.  PMM_F64_FUSED=1
+// / 0 forces either (read per call: tests compare both paths).
+constexpr double kF64FusedMinMatrixBytes = 256.0 * 1024.0 * 1024.0;
 bool f64_fused_enabled(int64_t m, int64_t n) {
   const char *e = getenv("PMM_F64_FUSED");
   if (e && *e) return atoi(e) != 0;

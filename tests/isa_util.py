@@ -22,6 +22,8 @@ BUILDS = [("pmm_bf16_ws_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] 
     ("pmm_bf16_ws_ks.hip", ("-DPMM_BF16_KS=6", "-DPMM_WS_NST=3")),
     ("pmm_bf16_ks.hip", ("-DPMM_BF16_KS=6",)),
 ] + [
+    # the 16x16x32 form of the wave-specialised kernel (PMM_WS_MFMA16)
+    ("pmm_bf16_ws_ks.hip", (f"-DPMM_BF16_KS={k}", "-DPMM_WS_MFMA16=1")) for k in (1, 2, 3, 6)] + [
     ("pmm_bf16_r64_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
     ("pmm_bf16_ff_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
     ("pmm_kernels.hip", ())]  # (the f32 seed prologue's asm LDS-DMA)
