@@ -1,9 +1,10 @@
 // pmm_bf16_ws_kernel.h -- wave-specialised bf16 fused GEMM + top-k kernel
 // (PMM_COMPUTE_BF16; BASELINE configs[3]: 100k x 1M x 768 bf16 cosine k=100).
 // Instantiated per padded-D step count by pmm_bf16_ks.hip; host side in
-// pmm_bf16.hip.  Same arithmetic and results as pmm_bf16_kernel.h (bf16
-// operands, f32 accumulation on v_mfma_f32_32x32x16_bf16, the f32 path's
-// metric epilogue, pre-filter, candidate buffers and merge).
+// pmm_bf16.hip.  bf16 operands, f32 accumulation on v_mfma_f32_16x16x32_bf16
+// with K in natural order (PMM_WS_MFMA16, below; the fire-and-forget kernel
+// runs the same chain and returns the same lists bit for bit), the f32
+// path's metric epilogue, pre-filter, candidate buffers and merge.
 //
 // Why a second bf16 kernel: at one wave per SIMD (pmm_bf16_kernel.h) every
 // latency of the top-k epilogue (LDS round trips, the survivors' exact
@@ -14,10 +15,12 @@
 //   * 4 MFMA waves (one per SIMD).  Wave w keeps its 32 query rows x D in
 //     registers for a whole work unit (192 registers at D = 768) and streams
 //     the corpus: per 64-column tile, KS K-steps of 128 bf16, each 8 substeps
-//     of two v_mfma_f32_32x32x16_bf16 with the corpus fragments read from LDS
-//     two substeps ahead (across K-step boundaries within a tile).  After a
-//     tile's K-loop it hands its 32 x 64 f32 accumulators to LDS (8
-//     ds_write_b128) and starts the next tile.
+//     of four v_mfma_f32_16x16x32_bf16 (two row blocks x two 16-column
+//     blocks; 32x32x16 pairs before round 4) with the corpus fragments read
+//     from LDS two substeps ahead (across K-step boundaries within a tile).
+//     After a tile's K-loop it hands its 32 x 64 f32 accumulators to LDS (8
+//     ds_write_b128, in the 32x32 accumulator layout the epilogue reads) and
+//     starts the next tile.
 //     No global memory traffic and no epilogue in this role.
 //   * 4 epilogue waves (one per SIMD).  Wave 4 + w owns wave w's 32 rows:
 //     their top-k state (threshold, candidate counts, LDS) has one owner.
@@ -115,7 +118,11 @@ constexpr int drain_tiles() { return KS == 1 ? (PMM_WS_DRAIN_TILES < 2 ? PMM_WS_
 #define PMM_WS_NST 7  // (A/B override: -DPMM_WS_NST=n)
 #endif
 #ifndef PMM_WS_MFMA16
-#define PMM_WS_MFMA16 0  // 1: the MFMA waves (and the seed) on v_mfma_f32_16x16x32_bf16
+// 1: the MFMA waves (and the seed) on v_mfma_f32_16x16x32_bf16 (default);
+// 0: on v_mfma_f32_32x32x16_bf16 with the K permuted inside each 128-wide
+// step (rounds 1-3).  c4 A/B, alternated on one box (profiles/r4_ws16/):
+// 143.0 / 142.9 vs 150.5 / 151.1 ms per kernel launch.
+#define PMM_WS_MFMA16 1
 #endif
 template <int KS>
 struct Carve {
@@ -780,9 +787,9 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
 // ===========================================================================
 // Threshold seed for the wave-specialised kernel.  The scores of the first ns
 // corpus rows, computed the way the main pass computes them -- the same query
-// fragments (registers), the same corpus K-chunk per lane and substep, the
-// same chain of v_mfma_f32_32x32x16_bf16 per 32-column block from
-// mfma_first, the same exact_score on the same norms -- so each is bit for
+// fragments (registers), the same corpus K-chunk per lane and step, the
+// same MFMA chain per accumulator block (16x16x32, or 32x32x16 with
+// PMM_WS_MFMA16=0), the same exact_score on the same norms -- so each is bit for
 // bit the score the main pass gives that (row, column).  Stored S[row][col]
 // (the main pass's candidate buffers, unused until it starts) for
 // seed_select_kernel, which sets gthr[row] = (k-th best composite) - 1: an
@@ -811,7 +818,9 @@ __global__ __launch_bounds__(256, 1) void seed_bf16_ws_kernel(GemmF32Args a, flo
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+#if !PMM_WS_MFMA16
   const int r32 = lane & 31, h = lane >> 5;
+#endif
   const int wrow0 = (int)blockIdx.x * BM + w * 32;
   // (wave-uniform; a wave past the last query row still stages and syncs)
   const bool active = wrow0 < a.M;

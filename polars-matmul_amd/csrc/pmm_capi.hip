@@ -24,13 +24,6 @@
 
 using namespace pmm;
 
-#ifndef PMM_LAB
-// The one-wave 256-row bf16 kernel is in the lab build only; never called
-// (bf16_r64_enabled is false outside it).
-hipError_t pmm::launch_gemm_bf16_r64(const GemmF32Args &, int, hipStream_t) { return hipErrorNotSupported; }
-size_t pmm::gemm_bf16_r64_lds_bytes(int) { return 0; }
-#endif
-
 namespace {
 
 constexpr const char *kVersion = "0.1.4+mi355x.r1";
@@ -332,23 +325,6 @@ bool bf16_ws_enabled(int capg, int64_t d) {
   return capg <= kBf16WsMaxCapg && gemm_bf16_ws_lds_bytes(capg, dp) <= 160 * 1024;
 }
 
-// One-wave-per-SIMD 256-row bf16 kernel (pmm_bf16_r64_kernel.h): lab build
-// only, PMM_BF16_R64=1 (read per call).  Measured slower than the
-// wave-specialised kernel at c4; kept as its bit-exact
-// cross-check.  It needs capg <= kBf16R64MaxCapg (k <= 192) and N < 2^26.
-bool bf16_r64_enabled(int64_t k, int64_t n, int64_t d) {
-#ifndef PMM_LAB
-  (void)k;
-  (void)n;
-  (void)d;
-  return false;
-#endif
-  const char *e = getenv("PMM_BF16_R64");
-  if (!e || atoi(e) == 0) return false;
-  const int dp = (int)(cdiv(d, kBf16DAlign) * kBf16DAlign);
-  return next_pow2((int)k + 64, 128) <= kBf16R64MaxCapg && n < (1 << 26) && gemm_bf16_r64_lds_bytes(dp) > 0 &&
-         gemm_bf16_r64_lds_bytes(dp) <= 160 * 1024;
-}
 
 
 // compute = PMM_COMPUTE_F32: the f32 kernel (variant chosen by LDS fit);
@@ -397,12 +373,10 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   }
   const bool bf16 = compute == PMM_COMPUTE_BF16;
   const bool ffk = bf16 && !t_no_ff && bf16_ff_enabled(k, n, d);
-  const bool r64 = bf16 && !ffk && bf16_r64_enabled(k, n, d);
-  if (r64) p.capg = next_pow2((int)k + 64, 128);  // (its compaction: 4 keys per lane)
-  const bool ws = bf16 && !ffk && !r64 && bf16_ws_enabled(p.capg, d);
-  p.variant = bf16 ? (ffk ? -6 : r64 ? -5 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
-  const int bm = bf16 ? (ffk ? kBf16FfBM : r64 ? kBf16R64BM : kBf16BM) : gemm_f32_bm(p.variant);
-  const int bn = bf16 ? (ffk ? kBf16FfBN : r64 ? kBf16R64BN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
+  const bool ws = bf16 && !ffk && bf16_ws_enabled(p.capg, d);
+  p.variant = bf16 ? (ffk ? -6 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
+  const int bm = bf16 ? (ffk ? kBf16FfBM : kBf16BM) : gemm_f32_bm(p.variant);
+  const int bn = bf16 ? (ffk ? kBf16FfBN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
   const size_t cand_budget = size_t(8) << 30;
   int64_t max_S = std::max<int64_t>(1, (int64_t)(cand_budget / std::max<size_t>(per_S, 1)));
@@ -419,12 +393,12 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   // f32 kernel: the same split of units (PMM_F32_WHOLE=0: split units only).
   // At c3 the GEMM time is unchanged (1076 ms either way) and the merge reads
   // 0.89 GB instead of 2.17 GB (0.40 vs 0.65 ms).
-  const bool whole = bf16 ? ((ws || r64) && !ffk && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
+  const bool whole = bf16 ? (ws && !ffk && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
   // unit overhead in tiles: loading the unit's query rows into registers
   // (Two 128 x 128 f32 workgroups per CU -- 196 registers and 74 KiB of LDS
   // let them co-reside -- planned for 512 slots measured slower at c1: 0.129
   // vs 0.118 ms, profiles/r3_c1/wpc_variant_ab.txt.)
-  plan_units(m, n, bm, bn, cus, bf16 ? (ffk || r64 ? 8.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
+  plan_units(m, n, bm, bn, cus, bf16 ? (ffk ? 8.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
   if (ffk) {
     // expected survivors of the guessed threshold per row, n j / ns, and per
     // (row, split); a row's count varies with the sample's j-th (a Gamma(j)
@@ -888,7 +862,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
       const int seed_env = getenv("PMM_BF16_SEED") ? atoi(getenv("PMM_BF16_SEED")) : 1;  // (read per call: tests toggle it)
       int64_t ns = kSeedMaxNs;
       if (const char *ne = getenv("PMM_SEED_NS")) ns = std::max<int64_t>(32, std::min<int64_t>(atoll(ne), kSeedMaxNs) / 32 * 32);
-      if (seed_env && (p.variant == -2 || p.variant == -5) && 4 * k <= ns && n >= 8 * ns &&
+      if (seed_env && p.variant == -2 && 4 * k <= ns && n >= 8 * ns &&
           (size_t)m * ns * 4 <= p.off_qn - p.off_cand) {
         float *sample = (float *)(w + p.off_cand);
         Timed t("seed_bf16", s);
@@ -922,13 +896,8 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
       }
     } else {
       // (the suffix names the kernel; pmm_timing_read matches substrings)
-      Timed t(p.variant == -5   ? "gemm_bf16_topk/r64"
-              : p.variant == -2 ? "gemm_bf16_topk/ws"
-                                : "gemm_bf16_topk/one-wave",
-              s);
-      HIP_TRY(p.variant == -5   ? launch_gemm_bf16_r64(a, p.grid, s)
-              : p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s)
-                                : launch_gemm_bf16(a, p.grid, s));
+      Timed t(p.variant == -2 ? "gemm_bf16_topk/ws" : "gemm_bf16_topk/one-wave", s);
+      HIP_TRY(p.variant == -2 ? launch_gemm_bf16_ws(a, p.grid, s) : launch_gemm_bf16(a, p.grid, s));
     }
     if (stats) {
       unsigned long long h[16];

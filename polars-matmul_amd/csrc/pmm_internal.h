@@ -154,15 +154,6 @@ hipError_t launch_gemm_bf16_ws(const GemmF32Args &a, int grid, hipStream_t s);
 // bf16 threshold seed (pmm_bf16_ws_kernel.h): S[row][0..ns) = the scores of
 // corpus rows 0..ns-1 exactly as the wave-specialised kernel computes them
 hipError_t launch_seed_bf16_ws(const GemmF32Args &a, float *S, int ns, hipStream_t s);
-// 256-query-row bf16 kernel held by one wave per SIMD (pmm_bf16_r64_kernel.h):
-// 64 rows x D per wave (AGPRs + VGPRs), 32-column corpus tiles, the epilogue
-// on the same wave between the MFMAs.  The wave-specialised kernel's
-// arithmetic bit for bit (its seed serves both).  capg <= kBf16R64MaxCapg,
-// N < 2^26.
-constexpr int kBf16R64BM = 256, kBf16R64BN = 32;
-constexpr int kBf16R64MaxCapg = 256;  // its compaction holds 4 keys per lane (k <= 192)
-size_t gemm_bf16_r64_lds_bytes(int D);  // D = padded dimension; 0 if unsupported
-hipError_t launch_gemm_bf16_r64(const GemmF32Args &a, int grid, hipStream_t s);
 // 256-query-row bf16 kernel on v_mfma_f32_16x16x32_bf16 with survivors stored
 // fire-and-forget against a static guessed threshold (pmm_bf16_ff_kernel.h):
 // 64 rows x D per wave, 32-column corpus tiles.  N < 2^26.

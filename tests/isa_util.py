@@ -14,17 +14,16 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-ffp-contract=off",
          "--cuda-device-only", "-S"]
 
 # (source, defines): every padded-D instantiation of the wave-specialised
-# kernel, the ring sizes whose slot sequence repeats per tile, the
-# one-wave-per-SIMD bf16 kernel at the largest D, every instantiation of the
-# 256-row one-wave kernel (lab build) and of the fire-and-forget 256-row one
+# kernel (and of its 32x32x16 form at a few), the ring sizes whose slot
+# sequence repeats per tile, the one-wave-per-SIMD bf16 kernel at the largest
+# D, every instantiation of the fire-and-forget 256-row kernel
 BUILDS = [("pmm_bf16_ws_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
     ("pmm_bf16_ws_ks.hip", ("-DPMM_BF16_KS=6", "-DPMM_WS_NST=6")),
     ("pmm_bf16_ws_ks.hip", ("-DPMM_BF16_KS=6", "-DPMM_WS_NST=3")),
     ("pmm_bf16_ks.hip", ("-DPMM_BF16_KS=6",)),
 ] + [
-    # the 16x16x32 form of the wave-specialised kernel (PMM_WS_MFMA16)
-    ("pmm_bf16_ws_ks.hip", (f"-DPMM_BF16_KS={k}", "-DPMM_WS_MFMA16=1")) for k in (1, 2, 3, 6)] + [
-    ("pmm_bf16_r64_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
+    # the 32x32x16 form of the wave-specialised kernel (PMM_WS_MFMA16=0)
+    ("pmm_bf16_ws_ks.hip", (f"-DPMM_BF16_KS={k}", "-DPMM_WS_MFMA16=0")) for k in (1, 2, 3, 6)] + [
     ("pmm_bf16_ff_ks.hip", (f"-DPMM_BF16_KS={k}",)) for k in range(1, 7)] + [
     ("pmm_kernels.hip", ())]  # (the f32 seed prologue's asm LDS-DMA)
 

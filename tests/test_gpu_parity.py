@@ -1169,61 +1169,61 @@ def test_set_devices_distinct_gpus(pmm, device_list, metric):
     assert np.array_equal(got[0], want[0])
 
 
-# ---- the one-wave-per-SIMD 256-row bf16 kernel (pmm_bf16_r64_kernel.h): in
-# the lab build only (measured slower than the shipped wave-specialised
-# kernel), kept as that kernel's bit-exact cross-check.  build()
-# builds libpmm_lab.so too; these tests load it beside libpmm.so through a
-# second binding of _native (its own ctypes handle; both libraries resolve
-# their own symbols) and compare its r64 lists with the SHIPPED kernel's, bit
-# for bit (indices and f32 scores), in the default GPU suite ----
-@pytest.fixture(scope="module")
-def lab(pmm):
-    import importlib.util
-
-    pkg = os.path.join(ROOT, "polars-matmul_amd", "polars_matmul")
-    so = os.path.join(pkg, "libpmm_lab.so")
-    assert os.path.exists(so), "libpmm_lab.so missing: run __graft_entry__.build() (it builds the lab library too)"
-    old = os.environ.get("PMM_LIB")
-    os.environ["PMM_LIB"] = "libpmm_lab.so"
-    try:
-        spec = importlib.util.spec_from_file_location("pmm_native_lab", os.path.join(pkg, "_native.py"))
-        mod = importlib.util.module_from_spec(spec)
-        spec.loader.exec_module(mod)
-    finally:
-        if old is None:
-            os.environ.pop("PMM_LIB", None)
-        else:
-            os.environ["PMM_LIB"] = old
-    assert mod.LIB_PATH.endswith("libpmm_lab.so") and mod.lib() is not _native().lib()
-    return mod
+# ---- the fire-and-forget 256-row bf16 kernel (pmm_bf16_ff_kernel.h,
+# PMM_BF16_FF=1): a different kernel structure (256 query rows on one wave per
+# SIMD, a guessed static threshold, survivors stored fire-and-forget, re-scored
+# and bucketed afterwards, unprovable rows re-run on the shipped kernel) over
+# the SAME MFMA chain as the shipped wave-specialised kernel
+# (v_mfma_f32_16x16x32_bf16 per 16 x 16 block, K in natural order), so the two
+# return the same lists bit for bit: the shipped kernel's cross-check (it
+# replaced the lab-only r64 kernel's, which ran the 32x32x16 chain).  Every
+# list also passes the bf16 truth check (the exact top-k of the rounded rows
+# up to f32 summation order). ----
+def _ws_and_ff(q, c, k, metric, monkeypatch, ff="1"):
+    monkeypatch.setenv("PMM_BF16_FF", ff)
+    fi, fsc = gpu_topk_bf16(q, c, k, metric)
+    monkeypatch.setenv("PMM_BF16_FF", "0")
+    wi, wsc = gpu_topk_bf16(q, c, k, metric)
+    return (fi, fsc), (wi, wsc)
 
 
-
-@pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (520, 40000, 768, 100), (70, 3000, 500, 192),
-                                     (257, 20011, 768, 100), (1, 1000, 256, 1), (600, 999, 700, 64),
-                                     (33, 70000, 128, 50), (130, 9000, 384, 120), (90, 5000, 640, 7)])
+@pytest.mark.parametrize("m,n,d,k", [(300, 70000, 256, 10), (520, 200000, 768, 100), (257, 131072, 384, 32),
+                                     (1000, 100003, 128, 20), (70, 90000, 640, 8), (33, 66000, 500, 16)])
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-def test_bf16_r64_equals_ws(pmm, lab, m, n, d, k, metric, monkeypatch):
-    rs = np.random.RandomState(m + n + d + k + 11)
+def test_bf16_ff_equals_ws(pmm, m, n, d, k, metric, monkeypatch):
+    rs = np.random.RandomState(m + n + d + k + 13)
     q = rs.randn(m, d).astype(np.float32)
     c = rs.randn(n, d).astype(np.float32)
     c[n // 2:n // 2 + 20] = c[:20]  # exact ties across the corpus
     q[m // 2] = 0.0                  # a zero-norm query row
-    monkeypatch.setenv("PMM_BF16_R64", "1")
-    ri, rsc = lab.topk_host(q, c, min(k, n), METRICS[metric], compute=lab.COMPUTE_BF16)
-    _bf16_truth_check(q, c, k, metric, ri, rsc, f"bf16 r64 {m}x{n}x{d} k={k} {metric}")
-    monkeypatch.setenv("PMM_BF16_R64", "0")
-    wi, wsc = gpu_topk_bf16(q, c, k, metric)  # the shipped library's kernel
-    assert np.array_equal(ri, wi)
-    assert np.array_equal(rsc.view(np.uint32), wsc.view(np.uint32))
+    (fi, fsc), (wi, wsc) = _ws_and_ff(q, c, k, metric, monkeypatch)
+    _bf16_truth_check(q, c, k, metric, fi, fsc, f"bf16 ff {m}x{n}x{d} k={k} {metric}")
+    assert np.array_equal(fi, wi)
+    assert np.array_equal(fsc.view(np.uint32), wsc.view(np.uint32))
+
+
+@pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (70, 3000, 500, 192), (257, 20011, 768, 100),
+                                     (1, 1000, 256, 1), (600, 999, 700, 64), (130, 9000, 384, 120)])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_bf16_ff_forced_equals_ws_small(pmm, m, n, d, k, metric, monkeypatch):
+    # corpora too short for the ff kernel's guess (PMM_BF16_FF=2 runs it
+    # anyway): most rows are re-run on the shipped kernel, the rest must
+    # match it bit for bit; odd D (zero-padded to 128), k up to 192, one row
+    rs = np.random.RandomState(m + n + d + k + 11)
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(n, d).astype(np.float32)
+    c[n // 2:n // 2 + 20] = c[:20]
+    q[m // 2] = 0.0
+    (fi, fsc), (wi, wsc) = _ws_and_ff(q, c, min(k, n), metric, monkeypatch, ff="2")
+    assert np.array_equal(fi, wi)
+    assert np.array_equal(fsc.view(np.uint32), wsc.view(np.uint32))
 
 
 @pytest.mark.parametrize("metric", ["cosine", "euclidean", "dot"])
-def test_bf16_r64_whole_blocks_and_splits(pmm, lab, metric, monkeypatch):
-    # PMM_CUS=16: 129 query blocks of 256 rows on 16 workgroups, so 128 run
-    # whole (row state carried across splits) and one as split units; the
-    # seed on (1M-scale thresholds are not needed for equality); bit-equal to
-    # the wave-specialised kernel on every row
+def test_bf16_ws_whole_blocks_equal_ff(pmm, metric, monkeypatch):
+    # PMM_CUS=16: 258 query blocks of 128 rows on 16 workgroups, so 256 run
+    # whole on the shipped kernel (row state carried across splits) and two
+    # as split units; the ff kernel runs split units only: bit-equal
     import torch
 
     monkeypatch.setenv("PMM_CUS", "16")
@@ -1231,15 +1231,15 @@ def test_bf16_r64_whole_blocks_and_splits(pmm, lab, metric, monkeypatch):
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(29)
-    m, N, d, k = 33000, 12000, 512, 40
+    m, N, d, k = 33000, 40000, 512, 40
     q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
     c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
     outs = []
-    for r64, lib in (("1", lab), ("0", n)):  # r64 (lab library), then the shipped ws kernel
-        monkeypatch.setenv("PMM_BF16_R64", r64)
+    for ff in ("2", "0"):
+        monkeypatch.setenv("PMM_BF16_FF", ff)
         oi = torch.empty((m, k), dtype=torch.int32, device=dev)
         osc = torch.empty((m, k), dtype=torch.float32, device=dev)
-        lib.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS[metric],
+        n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS[metric],
                            oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         outs.append((oi.cpu().numpy(), osc.cpu().numpy()))
@@ -1247,7 +1247,7 @@ def test_bf16_r64_whole_blocks_and_splits(pmm, lab, metric, monkeypatch):
     assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
 
 
-def test_bf16_r64_seeded_1m_rows_equal_ws(pmm, lab, monkeypatch):
+def test_bf16_ws_seeded_300k_rows_equal_ff(pmm, monkeypatch):
     # a corpus long enough for the threshold seed (n >= 8 ns) and for
     # compactions, queue overflows and catch-ups in early tiles: bit-equal
     import torch
@@ -1260,41 +1260,16 @@ def test_bf16_r64_seeded_1m_rows_equal_ws(pmm, lab, monkeypatch):
     q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
     c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
     outs = []
-    for r64, lib in (("1", lab), ("0", n)):  # r64 (lab library), then the shipped ws kernel
-        monkeypatch.setenv("PMM_BF16_R64", r64)
+    for ff in ("1", "0"):
+        monkeypatch.setenv("PMM_BF16_FF", ff)
         oi = torch.empty((m, k), dtype=torch.int32, device=dev)
         osc = torch.empty((m, k), dtype=torch.float32, device=dev)
-        lib.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS["cosine"],
+        n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS["cosine"],
                            oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         outs.append((oi.cpu().numpy(), osc.cpu().numpy()))
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
-
-
-# ---- the fire-and-forget 256-row bf16 kernel (pmm_bf16_ff_kernel.h,
-# PMM_BF16_FF=1): 16x16x32 MFMAs (a different f32 summation grouping than the
-# wave-specialised kernel's 32x32x16), a guessed static threshold, survivors
-# re-scored exactly and bucketed afterwards, rows it cannot prove exact re-run
-# on the wave-specialised kernel.  Every list passes the bf16 truth check
-# (the exact top-k of the rounded rows up to f32 summation order) and agrees
-# with the wave-specialised kernel but for near-ties ----
-@pytest.mark.parametrize("m,n,d,k", [(300, 70000, 256, 10), (520, 200000, 768, 100), (257, 131072, 384, 32),
-                                     (1000, 100003, 128, 20), (70, 90000, 640, 8), (33, 66000, 500, 16)])
-@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-def test_bf16_ff_vs_truth_and_ws(pmm, m, n, d, k, metric, monkeypatch):
-    rs = np.random.RandomState(m + n + d + k + 13)
-    q = rs.randn(m, d).astype(np.float32)
-    c = rs.randn(n, d).astype(np.float32)
-    c[n // 2:n // 2 + 20] = c[:20]  # exact ties across the corpus
-    q[m // 2] = 0.0                  # a zero-norm query row
-    monkeypatch.setenv("PMM_BF16_FF", "1")
-    fi, fsc = gpu_topk_bf16(q, c, k, metric)
-    _bf16_truth_check(q, c, k, metric, fi, fsc, f"bf16 ff {m}x{n}x{d} k={k} {metric}")
-    monkeypatch.setenv("PMM_BF16_FF", "0")
-    wi, wsc = gpu_topk_bf16(q, c, k, metric)
-    assert float(np.mean(fi == wi)) > 0.98
-    assert np.max(np.abs(fsc.astype(np.float64) - wsc)) < 1e-4 * max(1.0, float(np.max(np.abs(wsc))))
 
 
 @pytest.mark.parametrize("knobs", [{"PMM_FF_J": "1"}, {"PMM_FF_CAP": "256"}, {"PMM_FF_J": "1", "PMM_FF_CAP": "64"}])
@@ -1316,8 +1291,9 @@ def test_bf16_ff_reruns_rows_it_cannot_prove(pmm, knobs, metric, monkeypatch):
     for kk in knobs:
         monkeypatch.delenv(kk)
     monkeypatch.setenv("PMM_BF16_FF", "0")
-    wi, _ = gpu_topk_bf16(q, c, k, metric)
-    assert float(np.mean(fi == wi)) > 0.98
+    wi, wsc = gpu_topk_bf16(q, c, k, metric)
+    assert np.array_equal(fi, wi)
+    assert np.array_equal(fsc.view(np.uint32), wsc.view(np.uint32))
 
 
 def test_bf16_ff_device_api_whole_problem(pmm, monkeypatch):
@@ -1357,7 +1333,6 @@ def test_bf16_ws_d128_long_corpus_truth(pmm, m, metric, monkeypatch):
     # kernel's survivor drain must run before the column-norm ring overwrites
     # the queued survivors' norms (a 4-tile drain period did not: wrong cosine
     # and euclidean scores in sparsely surviving row groups)
-    monkeypatch.setenv("PMM_BF16_R64", "0")
     rs = np.random.RandomState(m + 5)
     q = rs.randn(m, 128).astype(np.float32)
     c = rs.randn(70000, 128).astype(np.float32)

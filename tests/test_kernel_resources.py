@@ -23,7 +23,7 @@ _LABEL = re.compile(r"^(\.LBB\S*:|; %bb\.\d+:)")
 
 
 def compiler_m0_uses(asm: str):
-    """Lines outside inline asm that name M0: the 256-row kernel (r64) sets M0
+    """Lines outside inline asm that name M0: the 256-row kernel (ff) sets M0
     in asm for its LDS-DMA (M0 cannot be declared clobbered), which is safe only
     while the compiler itself never relies on M0 in that kernel."""
     out, inasm, func = [], False, None
@@ -37,7 +37,7 @@ def compiler_m0_uses(asm: str):
             inasm = False
             continue
         s = line.strip()
-        if not inasm and func and ("r64" in func or "_ff_" in func) and not s.startswith(";") and re.search(r"\bm0\b", s):
+        if not inasm and func and "_ff_" in func and not s.startswith(";") and re.search(r"\bm0\b", s):
             out.append((func, s))
     return out
 
