@@ -1079,7 +1079,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="oracle baseline threads (0 = available_parallelism(), as faer's Rayon(0))")
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
-    ap.add_argument("--extra", default="c4,c1,c2,c1_f64,matmul",
+    ap.add_argument("--extra", default="c4,c1,c2,c1_f64,f64_large,matmul",
                     help="comma-separated secondary configs measured after the main line (N=1; 'none' = none; "
                          "'matmul' = .pmm.matmul at the c1 size; 'c1_f64' = the f64 top-k at the c1 size; "
                          "'f64_large' = the f64 top-k at 4096 x 1M x 256)")

@@ -374,6 +374,13 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   const bool bf16 = compute == PMM_COMPUTE_BF16;
   const bool ffk = bf16 && !t_no_ff && bf16_ff_enabled(k, n, d);
   const bool ws = bf16 && !ffk && bf16_ws_enabled(p.capg, d);
+  // the wave-specialised kernel on 16x16x32: twice the power of two (512 at
+  // k = 100) compacts less often; c4 alternated twice on one box: 131.0 /
+  // 130.5 vs 132.0 / 131.5 ms per launch (256: 135.4 / 135.0;
+  // profiles/r4_ws16/capg_ab.txt)
+  if (ws && !getenv("PMM_CAPG") && 2 * next_pow2((int)k + 64, 128) <= kBf16WsMaxCapg &&
+      bf16_ws_enabled(2 * next_pow2((int)k + 64, 128), d))
+    p.capg = 2 * next_pow2((int)k + 64, 128);
   p.variant = bf16 ? (ffk ? -6 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
   const int bm = bf16 ? (ffk ? kBf16FfBM : kBf16BM) : gemm_f32_bm(p.variant);
   const int bn = bf16 ? (ffk ? kBf16FfBN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
