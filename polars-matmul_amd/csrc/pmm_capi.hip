@@ -868,7 +868,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
       // the row's final k-th best: the main pass starts from it.
       const int seed_env = getenv("PMM_BF16_SEED") ? atoi(getenv("PMM_BF16_SEED")) : 1;  // (read per call: tests toggle it)
       int64_t ns = kSeedMaxNs;
-      if (const char *ne = getenv("PMM_SEED_NS")) ns = std::max<int64_t>(32, std::min<int64_t>(atoll(ne), kSeedMaxNs) / 32 * 32);
+      if (const char *ne = getenv("PMM_SEED_NS")) ns = std::max<int64_t>(32, std::min<int64_t>(atoll(ne), 4096) / 32 * 32);
       if (seed_env && p.variant == -2 && 4 * k <= ns && n >= 8 * ns &&
           (size_t)m * ns * 4 <= p.off_qn - p.off_cand) {
         float *sample = (float *)(w + p.off_cand);

@@ -901,13 +901,14 @@ __global__ __launch_bounds__(256) void seed_select_kernel(const float *__restric
 hipError_t launch_seed_select(const float *S, int64_t lds, int m, int ns, int k, int metric,
                               unsigned long long *gthr, hipStream_t s) {
   if (m <= 0) return hipSuccess;
-  // (up to 2048: the fire-and-forget bf16 kernel's guess sample)
-  if (ns > 2048 || k > ns) return hipErrorInvalidValue;
+  // (up to 4096: the bf16 seed sample and the fire-and-forget kernel's guess)
+  if (ns > 4096 || k > ns) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)((m + 3) / 4);
   if (ns <= 256) seed_select_kernel<4><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
   else if (ns <= 512) seed_select_kernel<8><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
   else if (ns <= 1024) seed_select_kernel<16><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
-  else seed_select_kernel<32><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
+  else if (ns <= 2048) seed_select_kernel<32><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
+  else seed_select_kernel<64><<<grid, 256, 0, s>>>(S, lds, m, ns, k, metric, gthr);
   return hipGetLastError();
 }
 

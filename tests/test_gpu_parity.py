@@ -775,7 +775,7 @@ def test_bf16_one_wave_per_simd_kernel(pmm, m, n, d, k, metric, monkeypatch):
 
 
 @pytest.mark.parametrize("m,n,d", [(300, 20000, 768), (140, 9000, 200), (70, 8200, 128), (64, 8500, 384),
-                                   (100, 9100, 512), (129, 8300, 640)])
+                                   (100, 9100, 512), (129, 8300, 640), (200, 40000, 256)])
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
 def test_bf16_seeded_threshold_is_exact(pmm, m, n, d, metric, monkeypatch):
     # the wave-specialised kernel starts each row from the k-th best of the
@@ -792,7 +792,8 @@ def test_bf16_seeded_threshold_is_exact(pmm, m, n, d, metric, monkeypatch):
     c[100, 5] = np.nan           # NaN scores inside the sample ...
     c[n - 3, 0] = np.nan         # ... and past it
     q[11, 2] = np.nan            # a query row whose every score is NaN
-    for k, ns in ((1, None), (10, None), (100, None), (256, None), (10, "64"), (50, "512")):
+    for k, ns in ((1, None), (10, None), (100, None), (256, None), (10, "64"), (50, "512"), (100, "2048"),
+                  (100, "4096")):  # (2048 / 4096: a seed only where n >= 8 ns)
         monkeypatch.setenv("PMM_BF16_SEED", "0")
         want = gpu_topk_bf16(q, c, k, metric)
         monkeypatch.setenv("PMM_BF16_SEED", "1")
