@@ -45,7 +45,7 @@ extern "C" {
 /* Arithmetic the top-k GEMM runs in (f32 inputs).  F32 = exact f32 MFMA
  * (v_mfma_f32_32x32x2_f32), the reference's precision.  BF16 = inputs rounded
  * to bf16 (round to nearest even) on device, products accumulated in f32
- * (v_mfma_f32_32x32x16_bf16), norms of the rounded rows in f32: the result is
+ * (v_mfma_f32_16x16x32_bf16), norms of the rounded rows in f32: the result is
  * the top-k of the bf16-rounded embeddings (BASELINE configs[3]); limits
  * d <= 768 and k <= 960 (PMM_ERR_UNSUPPORTED beyond). */
 #define PMM_COMPUTE_F32 0
@@ -145,10 +145,11 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
 /* The same f64 top-k on device rows (row strides >= roundup(d, 16), zero-
  * padded, 16-byte-aligned bases) on the caller's stream; out_idx / out_score
  * are device buffers of m*k entries, indices offset by index_base.  k <=
- * 1024: fused (f64 MFMA GEMM whose epilogue appends each element that beats
- * its row's running k-th to a candidate buffer, the corpus scanned in growing
- * column chunks with the k-th raised between chunks: no m x n matrix), else
- * (or when a row's buffer overflows) the materialised GEMM + row select.
+ * 1024 and an m x n score matrix of 256 MB or more: fused (f64 MFMA GEMM whose
+ * epilogue appends each element that beats its row's running k-th to a
+ * candidate buffer, the corpus scanned in growing column chunks with the k-th
+ * raised between chunks: no m x n matrix), else (or when a row's buffer
+ * overflows) the materialised GEMM + row select.
  * Synchronises the stream before returning (the overflow check). */
 int pmm_topk_f64_device(const double *q, int64_t ldq, int64_t m, const double *c, int64_t ldc, int64_t n,
                         int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *out_idx,
