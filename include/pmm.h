@@ -149,8 +149,9 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
  * epilogue appends each element that beats its row's running k-th to a
  * candidate buffer, the corpus scanned in growing column chunks with the k-th
  * raised between chunks: no m x n matrix), else (or when a row's buffer
- * overflows) the materialised GEMM + row select.
- * Synchronises the stream before returning (the overflow check). */
+ * overflows) the materialised GEMM + row select.  The fused scan
+ * synchronises the stream before returning (its overflow check); the
+ * materialised path returns with the work queued on the stream. */
 int pmm_topk_f64_device(const double *q, int64_t ldq, int64_t m, const double *c, int64_t ldc, int64_t n,
                         int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *out_idx,
                         double *out_score, void *stream);
