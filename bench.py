@@ -605,11 +605,11 @@ def kernel_stats(bf16):
         # which bf16 kernel ran (the library's timer names carry it); the
         # fire-and-forget kernel's re-run rows go through the ws kernel, timed
         # apart from it (per step, not per launch)
-        out["bf16_kernel"] = next((v for v in ("ff", "fire-ws", "ws", "one-wave")
+        out["bf16_kernel"] = next((v for v in ("ff", "ws", "one-wave")
                                    if _native.timing_read("gemm_bf16_topk/" + v)[1]), "ws")
         ms, n = _native.timing_read("gemm_bf16_topk/" + out["bf16_kernel"])
         out["gemm"] = (ms / n if n else None, n)
-        if out["bf16_kernel"] in ("ff", "fire-ws"):
+        if out["bf16_kernel"] == "ff":
             rms, rn = _native.timing_read("gemm_bf16_topk/ws")
             out["ff_rerun"] = (rms, rn)
     return out
@@ -618,9 +618,6 @@ def kernel_stats(bf16):
 BF16_KERNEL_NAMES = {
     "ff": "gemm_bf16_ff_kernel (256 query rows per CU on 16x16x32 MFMAs, pre-filter against a guessed "
           "static threshold, survivors stored fire-and-forget; + seed_bf16_ws_kernel in achieved)",
-    "fire-ws": "gemm_bf16_ws_kernel, fire-and-forget mode (wave-specialised GEMM on 16x16x32 MFMAs, survivors of "
-               "a guessed static threshold appended to HBM, re-scored and bucketed by ff_bucket_kernel; "
-               "+ seed_bf16_ws_kernel in achieved)",
     "ws": "gemm_bf16_ws_kernel (wave-specialised fused GEMM + metric + top-k on 16x16x32 MFMAs; "
           "+ seed_bf16_ws_kernel in achieved)",
     "one-wave": "gemm_bf16_kernel (one-wave fused GEMM + metric + top-k)",

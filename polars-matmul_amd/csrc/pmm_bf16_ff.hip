@@ -48,8 +48,7 @@ hipError_t launch_gemm_bf16_ff(const GemmF32Args &a, int grid, hipStream_t s) {
 
 // ---------------------------------------------------------------------------
 // Bucketing pass: workgroup (query block qb, wave w) takes the S regions of
-// its rpr rows (one per split unit; 64 for this kernel's waves, 32 for the
-// wave-specialised kernel's fire-and-forget mode), re-scores every item exactly -- the
+// its 64 rows (one per split unit), re-scores every item exactly -- the
 // reference's operation order on the main pass's raw dot (exact_score) --
 // keeps those whose composite key beats the row's threshold (the guess - 1)
 // and appends them to the row's candidate list of that split (LDS counters).
@@ -57,22 +56,22 @@ hipError_t launch_gemm_bf16_ff(const GemmF32Args &a, int grid, hipStream_t s) {
 // dropped (no region or list overflow); the others are listed for a re-run.
 // ---------------------------------------------------------------------------
 template <int METRIC>
-__global__ __launch_bounds__(256) void ff_bucket_kernel(GemmF32Args a, int rpr, unsigned *fb_count, int *fb_rows) {
+__global__ __launch_bounds__(256) void ff_bucket_kernel(GemmF32Args a, unsigned *fb_count, int *fb_rows) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr bool XFORM = METRIC != kMetricDot;
-  unsigned *cnt_l = (unsigned *)smem;         // [rpr][S]
-  int *bad_l = (int *)(cnt_l + rpr * a.S);    // [rpr]
+  unsigned *cnt_l = (unsigned *)smem;        // [64][S]
+  int *bad_l = (int *)(cnt_l + 64 * a.S);    // [64]
   const int tid = threadIdx.x;
   const int qb = (int)blockIdx.x / ff::NW, w = (int)blockIdx.x % ff::NW;
-  const int wrow0 = qb * ff::NW * rpr + w * rpr;
-  for (int i = tid; i < rpr * a.S; i += 256) cnt_l[i] = 0u;
-  if (tid < rpr) bad_l[tid] = 0;
+  const int wrow0 = qb * ff::BM + w * ff::RW;
+  for (int i = tid; i < 64 * a.S; i += 256) cnt_l[i] = 0u;
+  if (tid < 64) bad_l[tid] = 0;
   __syncthreads();
   for (int s = 0; s < a.S; s++) {
     const int64_t r = (int64_t)(s * a.QB + qb) * ff::NW + w;
     const unsigned n = a.ffcnt[r];
     if (n > (unsigned)a.ffcap) {  // items were dropped: every row of the region re-runs
-      if (tid < rpr) bad_l[tid] = 1;
+      if (tid < 64) bad_l[tid] = 1;
     }
     const unsigned nn = n < (unsigned)a.ffcap ? n : (unsigned)a.ffcap;
     const unsigned long long *reg = a.ffreg + r * a.ffcap;
@@ -82,7 +81,7 @@ __global__ __launch_bounds__(256) void ff_bucket_kernel(GemmF32Args a, int rpr, 
       const uint32_t hi = (uint32_t)(it >> 32);
       const int row = (int)(hi >> 26), col = (int)(hi & 0x3FFFFFFu);
       const int grow = wrow0 + row;
-      if (grow >= a.M || col >= a.N) continue;
+      if (grow >= a.M) continue;
       const float sc = exact_score<METRIC>(v, XFORM ? a.qn[grow] : 0.0f, XFORM ? a.cn[col] : 0.0f);
       const u64 comp = ((u64)okey32(METRIC == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~(uint32_t)col);
       if (comp > a.gthr[grow]) {
@@ -92,7 +91,7 @@ __global__ __launch_bounds__(256) void ff_bucket_kernel(GemmF32Args a, int rpr, 
     }
   }
   __syncthreads();
-  if (tid < rpr) {
+  if (tid < 64) {
     const int grow = wrow0 + tid;
     if (grow < a.M) {
       unsigned tot = 0;
@@ -112,13 +111,12 @@ __global__ __launch_bounds__(256) void ff_bucket_kernel(GemmF32Args a, int rpr, 
   }
 }
 
-hipError_t launch_ff_bucket(const GemmF32Args &a, int rpr, unsigned *fb_count, int *fb_rows, hipStream_t s) {
+hipError_t launch_ff_bucket(const GemmF32Args &a, unsigned *fb_count, int *fb_rows, hipStream_t s) {
   if (a.M <= 0) return hipSuccess;
-  if (rpr < 1 || rpr > 64) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)(a.QB * ff::NW);
   // (many splits per query block -- few query rows over a long corpus -- take
   // more than the default 64 KiB of counters)
-  const size_t lds = (size_t)rpr * a.S * 4 + (size_t)rpr * 4;
+  const size_t lds = (size_t)64 * a.S * 4 + 64 * 4;
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (lds > 64 * 1024) {
     static bool attr_set[3] = {false, false, false};
@@ -131,9 +129,9 @@ hipError_t launch_ff_bucket(const GemmF32Args &a, int rpr, unsigned *fb_count, i
       attr_set[a.metric] = true;
     }
   }
-  if (a.metric == kMetricCosine) ff_bucket_kernel<kMetricCosine><<<grid, 256, lds, s>>>(a, rpr, fb_count, fb_rows);
-  else if (a.metric == kMetricDot) ff_bucket_kernel<kMetricDot><<<grid, 256, lds, s>>>(a, rpr, fb_count, fb_rows);
-  else ff_bucket_kernel<kMetricEuclidean><<<grid, 256, lds, s>>>(a, rpr, fb_count, fb_rows);
+  if (a.metric == kMetricCosine) ff_bucket_kernel<kMetricCosine><<<grid, 256, lds, s>>>(a, fb_count, fb_rows);
+  else if (a.metric == kMetricDot) ff_bucket_kernel<kMetricDot><<<grid, 256, lds, s>>>(a, fb_count, fb_rows);
+  else ff_bucket_kernel<kMetricEuclidean><<<grid, 256, lds, s>>>(a, fb_count, fb_rows);
   return hipGetLastError();
 }
 

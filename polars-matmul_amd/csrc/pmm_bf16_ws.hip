@@ -49,13 +49,9 @@ hipError_t launch_seed_bf16_ws(const GemmF32Args &a, float *S, int ns, hipStream
 hipError_t launch_gemm_bf16_ws(const GemmF32Args &a, int grid, hipStream_t s) {
   const size_t lds = gemm_bf16_ws_lds_bytes(a.capg, a.D);
   // the kernel's grid and tile shapes assume: whole 128-wide K-steps, a
-  // capacity the LDS carve holds (compactions; none in the fire-and-forget
-  // mode, which runs split units only, with regions to append to and columns
-  // that fit the items' 26 bits), and every unit's tiles inside the corpus
-  const bool ffa = a.ffreg != nullptr;
-  if (lds > 160 * 1024 || a.D % kBf16DAlign != 0 || (!ffa && a.capg > kBf16WsMaxCapg) || a.tps < 1 ||
-      (int64_t)a.ntiles * ws::BN < a.N || (int64_t)a.QB * ws::BM < a.M ||
-      (ffa && (a.qb_full != 0 || !a.ffcnt || a.ffcap < 1 || a.N >= (1 << 26))))
+  // capacity the LDS carve holds, and every unit's tiles inside the corpus
+  if (lds > 160 * 1024 || a.D % kBf16DAlign != 0 || a.capg > kBf16WsMaxCapg || a.tps < 1 ||
+      (int64_t)a.ntiles * ws::BN < a.N || (int64_t)a.QB * ws::BM < a.M)
     return hipErrorInvalidValue;
   switch (a.D / 128) {
     case 1: return launch_bf16_ws_ks1(a, grid, lds, s);

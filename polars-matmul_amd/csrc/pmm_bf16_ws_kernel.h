@@ -168,22 +168,6 @@ __device__ __forceinline__ void wait_vm_n(int n) {
     default: wait_vm<0>(); break;  // (never taken; safe)
   }
 }
-// any count 0..63 (clamped: a smaller count only waits longer)
-__device__ __forceinline__ void wait_vm_any(int n) {
-  switch (n < 0 ? 0 : (n > 63 ? 63 : n)) {
-#define PMM_WANY(N) \
-  case N: wait_vm<N>(); break;
-    PMM_WANY(0) PMM_WANY(1) PMM_WANY(2) PMM_WANY(3) PMM_WANY(4) PMM_WANY(5) PMM_WANY(6) PMM_WANY(7)
-    PMM_WANY(8) PMM_WANY(9) PMM_WANY(10) PMM_WANY(11) PMM_WANY(12) PMM_WANY(13) PMM_WANY(14) PMM_WANY(15)
-    PMM_WANY(16) PMM_WANY(17) PMM_WANY(18) PMM_WANY(19) PMM_WANY(20) PMM_WANY(21) PMM_WANY(22) PMM_WANY(23)
-    PMM_WANY(24) PMM_WANY(25) PMM_WANY(26) PMM_WANY(27) PMM_WANY(28) PMM_WANY(29) PMM_WANY(30) PMM_WANY(31)
-    PMM_WANY(32) PMM_WANY(33) PMM_WANY(34) PMM_WANY(35) PMM_WANY(36) PMM_WANY(37) PMM_WANY(38) PMM_WANY(39)
-    PMM_WANY(40) PMM_WANY(41) PMM_WANY(42) PMM_WANY(43) PMM_WANY(44) PMM_WANY(45) PMM_WANY(46) PMM_WANY(47)
-    PMM_WANY(48) PMM_WANY(49) PMM_WANY(50) PMM_WANY(51) PMM_WANY(52) PMM_WANY(53) PMM_WANY(54) PMM_WANY(55)
-    PMM_WANY(56) PMM_WANY(57) PMM_WANY(58) PMM_WANY(59) PMM_WANY(60) PMM_WANY(61) PMM_WANY(62) PMM_WANY(63)
-#undef PMM_WANY
-  }
-}
 __device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 template <int N>
 __device__ __forceinline__ void wait_lgkm() {
@@ -303,14 +287,7 @@ __device__ __forceinline__ bool unit_at(const GemmF32Args &a, int round, UnitPos
 // ===========================================================================
 // KS = padded D / 128 (K-steps per tile).
 // ===========================================================================
-// FFA (fire-and-forget appends): the epilogue waves pre-filter against each
-// row's STATIC threshold (gthr: a guess, the j-th best of an exact sample)
-// and append every survivor -- raw dot, row, column -- to this (unit, wave)'s
-// HBM region (a.ffreg / a.ffcnt, the layout of the fire-and-forget 256-row
-// kernel's: ff_bucket_kernel re-scores and buckets them afterwards), with no
-// LDS queue, no exact re-score, no candidate buffers and no compactions on
-// the epilogue waves; split units only (a.qb_full == 0).
-template <int KS, int METRIC, bool FFA>
+template <int KS, int METRIC>
 __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a) {
   using namespace ws;
   using C = Carve<KS>;
@@ -584,18 +561,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       const uint32_t lq_lds = (uint32_t)(size_t)(LDS_AS char *)(smem + C::OFF_QUEUE) + rw * QCAP * 8;
       const u64 *lq = (const u64 *)(smem + C::OFF_QUEUE) + rw * QCAP;
       int qlen = 0;  // wave-uniform
-      // FFA: this (unit, wave)'s survivor region and its running count
-      // (wave-uniform; past ffcap the last slot is overwritten and the count
-      // runs on, so the bucketing pass re-runs the region's rows), and the
-      // store instructions issued in the current interval and the NST - 2
-      // before it: each is younger than the ring DMA a vmcnt wait targets
-      unsigned long long *reg = nullptr;
-      unsigned nreg = 0;
-      int st0 = 0, st1 = 0, st2 = 0, st3 = 0, st4 = 0, st5 = 0;
-      static_assert(!FFA || NST <= 8, "FFA store counts cover NST - 2 <= 6 intervals");
-      if constexpr (FFA) reg = a.ffreg + ((int64_t)(u.s * a.QB + u.qb) * NWE + rw) * a.ffcap;
       auto drain = [&]() __attribute__((always_inline)) {
-        if constexpr (FFA) return;
         const uint64_t td0 = stamp();
         if (timing) nq += (uint64_t)qlen;
         for (int base = 0; base < qlen; base += 64) {
@@ -673,21 +639,6 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
           const bool act = bits != 0u;
           const u64 mk = __ballot(act);
           if (mk == 0ull) break;
-          if constexpr (FFA) {
-            // one store instruction per round (every lane with a survivor
-            // stores; an overflowing slot is clamped to the last one)
-            if (act) {
-              const int j = 31 - __builtin_clz(bits);
-              bits &= ~(1u << j);
-              const int e = 15 - j;
-              const float v = hf[(e >> 2) * 256 + (e & 3)];
-              const uint32_t hi = ((uint32_t)acc_row(e, h) << 26) | (uint32_t)gcol;
-              const unsigned slot = min(nreg + (unsigned)lanes_below(mk), (unsigned)a.ffcap - 1u);
-              reg[slot] = ((u64)hi << 32) | (u64)__float_as_uint(v);
-            }
-            nreg += (unsigned)__popcll(mk);
-            st0++;
-          } else {
           if (act) {
             const int j = 31 - __builtin_clz(bits);  // bit j <-> e = 15 - j
             bits &= ~(1u << j);
@@ -703,7 +654,6 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
           if (qlen > QCAP - 64) {
             wait_lgkm0();
             drain();
-          }
           }
         }
         if (timing) cy5 += stamp() - tq0;
@@ -790,25 +740,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             int n = 0;
 #pragma unroll
             for (int j = 2 + LEAD; j < NST; j++) n += step_dmas<XFORM>((ks + j) % KS);
-            if constexpr (FFA) {
-              // + the stores issued since that step's DMA: in this interval and
-              // the NST - 3 before it (its DMA went out NST - 2 intervals ago)
-              int sn = st0;
-              if (NST - 3 >= 1) sn += st1;
-              if (NST - 3 >= 2) sn += st2;
-              if (NST - 3 >= 3) sn += st3;
-              if (NST - 3 >= 4) sn += st4;
-              if (NST - 3 >= 5) sn += st5;
-              wait_vm_any(n + sn);
-              st5 = st4;
-              st4 = st3;
-              st3 = st2;
-              st2 = st1;
-              st1 = st0;
-              st0 = 0;
-            } else {
-              wait_vm_n(n);
-            }
+            wait_vm_n(n);
           }
           if (timing) cy2 += stamp() - tt;
           sl = (sl == NST - 1) ? 0 : sl + 1;
@@ -822,9 +754,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
         drain();
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // ring DMAs past the unit's end
-      if constexpr (FFA) {
-        if (lane == 0) a.ffcnt[(int64_t)(u.s * a.QB + u.qb) * NWE + rw] = nreg;
-      } else if (lane < 32) {
+      if (lane < 32) {
         const int grow = wrow0 + lane;
         if (u.last && grow < a.M) a.cnt[(int64_t)grow * a.S + s] = cnt_w[lane];
       }
@@ -1029,16 +959,16 @@ static hipError_t launch_seed_bf16_ws_t(const GemmF32Args &a, float *S, int ns, 
   return hipGetLastError();
 }
 
-template <int KS, int METRIC, bool FFA>
+template <int KS, int METRIC>
 static hipError_t launch_bf16_ws_t(const GemmF32Args &a, int grid, size_t lds, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)gemm_bf16_ws_kernel<KS, METRIC, FFA>,
+    hipError_t e = hipFuncSetAttribute((const void *)gemm_bf16_ws_kernel<KS, METRIC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  gemm_bf16_ws_kernel<KS, METRIC, FFA><<<dim3(grid), dim3(ws::NTH), lds, s>>>(a);
+  gemm_bf16_ws_kernel<KS, METRIC><<<dim3(grid), dim3(ws::NTH), lds, s>>>(a);
   return hipGetLastError();
 }
 

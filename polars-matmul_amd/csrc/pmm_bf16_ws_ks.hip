@@ -12,15 +12,9 @@ namespace pmm {
 #define PMM_CAT(a, b) PMM_CAT2(a, b)
 hipError_t PMM_CAT(launch_bf16_ws_ks, PMM_BF16_KS)(const GemmF32Args &a, int grid, size_t lds,
                                                   hipStream_t s) {
-  // (a.ffreg set: the fire-and-forget epilogue)
-  if (a.ffreg) {
-    if (a.metric == kMetricCosine) return launch_bf16_ws_t<PMM_BF16_KS, kMetricCosine, true>(a, grid, lds, s);
-    if (a.metric == kMetricDot) return launch_bf16_ws_t<PMM_BF16_KS, kMetricDot, true>(a, grid, lds, s);
-    return launch_bf16_ws_t<PMM_BF16_KS, kMetricEuclidean, true>(a, grid, lds, s);
-  }
-  if (a.metric == kMetricCosine) return launch_bf16_ws_t<PMM_BF16_KS, kMetricCosine, false>(a, grid, lds, s);
-  if (a.metric == kMetricDot) return launch_bf16_ws_t<PMM_BF16_KS, kMetricDot, false>(a, grid, lds, s);
-  return launch_bf16_ws_t<PMM_BF16_KS, kMetricEuclidean, false>(a, grid, lds, s);
+  if (a.metric == kMetricCosine) return launch_bf16_ws_t<PMM_BF16_KS, kMetricCosine>(a, grid, lds, s);
+  if (a.metric == kMetricDot) return launch_bf16_ws_t<PMM_BF16_KS, kMetricDot>(a, grid, lds, s);
+  return launch_bf16_ws_t<PMM_BF16_KS, kMetricEuclidean>(a, grid, lds, s);
 }
 
 hipError_t PMM_CAT(launch_seed_bf16_ws_ks, PMM_BF16_KS)(const GemmF32Args &a, float *S, int ns,

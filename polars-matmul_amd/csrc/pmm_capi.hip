@@ -350,26 +350,6 @@ bool bf16_ff_enabled(int64_t k, int64_t n, int64_t d) {
          gemm_bf16_ff_lds_bytes(dp) > 0 && gemm_bf16_ff_lds_bytes(dp) <= 160 * 1024;
 }
 
-// The wave-specialised kernel's fire-and-forget mode (FFA in
-// pmm_bf16_ws_kernel.h; variant -7): the epilogue waves append survivors of a
-// static guessed threshold (the j-th best of an exact ns-column sample) to
-// HBM regions instead of queueing, re-scoring and compacting them;
-// ff_bucket_kernel re-scores and buckets them, rows it cannot prove exact are
-// re-run.  PMM_BF16_WSFF=1 where the guess applies (about n j / ns >= 4 k
-// scores per row), 2 (tests) wherever it can run, 0 never; PMM_WSFF_J sets j.
-int wsff_guess_j() {
-  const char *e = getenv("PMM_WSFF_J");
-  return e ? std::max(1, atoi(e)) : 3;
-}
-bool bf16_wsff_enabled(int64_t k, int64_t n) {
-  const char *e = getenv("PMM_BF16_WSFF");
-  const int mode = e ? atoi(e) : 0;
-  if (mode == 0) return false;
-  const int64_t ns = ff_guess_ns(n);
-  const bool guess_ok = (double)n * wsff_guess_j() / (double)ns >= 4.0 * (double)k;
-  return ns >= 256 && ns >= wsff_guess_j() && (guess_ok || mode == 2) && k + 64 <= 8192 && n < (1 << 26);
-}
-
 int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p,
               int compute = PMM_COMPUTE_F32) {
   // testing knob: plan for fewer workgroups (small problems then take the
@@ -401,8 +381,7 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   if (ws && !getenv("PMM_CAPG") && 2 * next_pow2((int)k + 64, 128) <= kBf16WsMaxCapg &&
       bf16_ws_enabled(2 * next_pow2((int)k + 64, 128), d))
     p.capg = 2 * next_pow2((int)k + 64, 128);
-  const bool wsff = ws && !t_no_ff && bf16_wsff_enabled(k, n);
-  p.variant = bf16 ? (ffk ? -6 : wsff ? -7 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
+  p.variant = bf16 ? (ffk ? -6 : ws ? -2 : -1) : choose_variant(0, p.capg, m, n, cus);
   const int bm = bf16 ? (ffk ? kBf16FfBM : kBf16BM) : gemm_f32_bm(p.variant);
   const int bn = bf16 ? (ffk ? kBf16FfBN : ws ? kBf16WsBN : kBf16BN) : gemm_f32_bn(p.variant);
   const size_t per_S = (size_t)m * p.capg * 8 + (size_t)m * 4;
@@ -421,25 +400,24 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   // f32 kernel: the same split of units (PMM_F32_WHOLE=0: split units only).
   // At c3 the GEMM time is unchanged (1076 ms either way) and the merge reads
   // 0.89 GB instead of 2.17 GB (0.40 vs 0.65 ms).
-  const bool whole = bf16 ? (ws && !ffk && !wsff && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
+  const bool whole = bf16 ? (ws && !ffk && !(we && atoi(we) == 0)) : !(fe && atoi(fe) == 0);
   // unit overhead in tiles: loading the unit's query rows into registers
   // (Two 128 x 128 f32 workgroups per CU -- 196 registers and 74 KiB of LDS
   // let them co-reside -- planned for 512 slots measured slower at c1: 0.129
   // vs 0.118 ms, profiles/r3_c1/wpc_variant_ab.txt.)
   plan_units(m, n, bm, bn, cus, bf16 ? (ffk ? 8.0 : ws ? 4.0 : 2.0) : 0.5, max_S, p, whole);
-  if (ffk || wsff) {
+  if (ffk) {
     // expected survivors of the guessed threshold per row, n j / ns, and per
     // (row, split); a row's count varies with the sample's j-th (a Gamma(j)
-    // quantile: 3x the mean is rare), a region's (64 or 32 rows) much less
+    // quantile: 3x the mean is rare), a region's (64 rows) much less
     p.ff_ns = (int)ff_guess_ns(n);
-    p.ff_j = ffk ? ff_guess_j() : wsff_guess_j();
-    const double rpr = ffk ? 64.0 : 32.0;  // rows per survivor region
+    p.ff_j = ff_guess_j();
     const double e_row = (double)n * p.ff_j / p.ff_ns;
     const double e_rs = e_row * std::min<double>(1.0, (double)p.tps * bn / (double)n);
     p.capg = (int)std::max<int64_t>(k + 64, ((int64_t)(3.0 * e_rs) + 64 + 63) / 64 * 64);
     // (the seed's sample of ns scores per row lives in the candidate lists)
     p.capg = (int)std::max<int64_t>(p.capg, cdiv((int64_t)p.ff_ns, 2 * p.S));
-    p.ffcap = (int)(((int64_t)(1.5 * rpr * e_rs) + 256 + 63) / 64 * 64);
+    p.ffcap = (int)(((int64_t)(1.5 * 64.0 * e_rs) + 256 + 63) / 64 * 64);
     if (const char *ce = getenv("PMM_FF_CAP")) p.ffcap = std::max(64, atoi(ce));  // (tests: force overflows)
   }
   // merge_kernel's per-row LDS capacity: at least 512, so a row's candidate
@@ -461,7 +439,7 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   off = al256(off + (metric != kMetricDot ? (size_t)n * 8 : 0));
   p.off_wq = off;  // f32 kernel: per-wave survivor queues, grid x waves x (32 x BN) u64
   off = al256(off + (bf16 ? 0 : (size_t)p.grid * (bm / 32) * 32 * bn * 8));
-  if (ffk || wsff) {
+  if (ffk) {
     p.off_ffcnt = off;  // [units][4 waves]
     off = al256(off + (size_t)p.units * 4 * 4);
     p.off_ffreg = off;  // [units][4 waves][ffcap]
@@ -899,10 +877,9 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
         HIP_TRY(launch_seed_select(sample, ns, (int)m, (int)ns, (int)k, metric, a.gthr, s));
       }
     }
-    if (p.variant == -6 || p.variant == -7) {
-      // fire-and-forget 256-row kernel, or the wave-specialised kernel's
-      // fire-and-forget mode: the guessed threshold (the j-th best of an
-      // exact ns-row sample, minus 1), the pass, the exact re-score and
+    if (p.variant == -6) {
+      // fire-and-forget 256-row kernel: the guessed threshold (the j-th best
+      // of an exact ns-row sample, minus 1), the pass, the exact re-score and
       // bucketing into the candidate lists; rows it cannot prove exact are
       // re-run below
       float *sample = (float *)(w + p.off_cand);
@@ -915,19 +892,14 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
       a.ffreg = (unsigned long long *)(w + p.off_ffreg);
       a.ffcnt = (unsigned *)(w + p.off_ffcnt);
       a.ffcap = p.ffcap;
-      if (p.variant == -6) {
+      {
         Timed t("gemm_bf16_topk/ff", s);
         HIP_TRY(launch_gemm_bf16_ff(a, p.grid, s));
-      } else {
-        // (a label that is no substring of the others: pmm_timing_read matches substrings)
-        Timed t("gemm_bf16_topk/fire-ws", s);
-        HIP_TRY(launch_gemm_bf16_ws(a, p.grid, s));
       }
       HIP_TRY(hipMemsetAsync(w + p.off_fb, 0, 16, s));
       {
         Timed t("ff_bucket", s);
-        HIP_TRY(launch_ff_bucket(a, p.variant == -6 ? kBf16FfBM / 4 : kBf16BM / 4,
-                                 (unsigned *)(w + p.off_fb), (int *)(w + p.off_fb + 16), s));
+        HIP_TRY(launch_ff_bucket(a, (unsigned *)(w + p.off_fb), (int *)(w + p.off_fb + 16), s));
       }
     } else {
       // (the suffix names the kernel; pmm_timing_read matches substrings)
@@ -972,7 +944,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     Timed t("merge_topk", s);
     HIP_TRY(launch_merge(ma, 0, s));
   }
-  if (p.variant == -6 || p.variant == -7) {
+  if (p.variant == -6) {
     int rc = ff_rerun(q, ldq, m, c, ldc, n, d, k, metric, index_base, out_idx, out_score,
                       (const unsigned *)(w + p.off_fb), s, dev);
     if (rc) return rc;

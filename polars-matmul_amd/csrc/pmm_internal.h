@@ -169,8 +169,7 @@ hipError_t launch_ff_gather_rows(const uint16_t *q, int64_t ldq, const int *rows
                                  hipStream_t s);
 hipError_t launch_ff_scatter_lists(const uint32_t *oi, const float *os, const int *rows, int r, int k,
                                    uint32_t *out_idx, float *out_score, hipStream_t s);
-hipError_t launch_ff_bucket(const GemmF32Args &a, int rows_per_region, unsigned *fb_count, int *fb_rows,
-                            hipStream_t s);
+hipError_t launch_ff_bucket(const GemmF32Args &a, unsigned *fb_count, int *fb_rows, hipStream_t s);
 // f32 rows -> bf16 (round to nearest even) with row stride ldd, columns
 // d..ldd-1 zero-filled.
 hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t lds, uint16_t *dst,

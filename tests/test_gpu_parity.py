@@ -1180,76 +1180,12 @@ def test_set_devices_distinct_gpus(pmm, device_list, metric):
 # replaced the lab-only r64 kernel's, which ran the 32x32x16 chain).  Every
 # list also passes the bf16 truth check (the exact top-k of the rounded rows
 # up to f32 summation order). ----
-def _ws_and_ff(q, c, k, metric, monkeypatch, ff="1", var="PMM_BF16_FF"):
-    monkeypatch.setenv(var, ff)
+def _ws_and_ff(q, c, k, metric, monkeypatch, ff="1"):
+    monkeypatch.setenv("PMM_BF16_FF", ff)
     fi, fsc = gpu_topk_bf16(q, c, k, metric)
-    monkeypatch.setenv(var, "0")
+    monkeypatch.setenv("PMM_BF16_FF", "0")
     wi, wsc = gpu_topk_bf16(q, c, k, metric)
     return (fi, fsc), (wi, wsc)
-
-
-# the wave-specialised kernel's own fire-and-forget mode (PMM_BF16_WSFF: the
-# same MFMA waves, the epilogue waves appending survivors of a guessed static
-# threshold to HBM, ff_bucket_kernel re-scoring them, unprovable rows re-run):
-# the same lists as the default mode, bit for bit
-@pytest.mark.parametrize("m,n,d,k", [(300, 70000, 256, 10), (520, 200000, 768, 100), (257, 131072, 384, 32),
-                                     (1000, 100003, 128, 20), (70, 90000, 640, 8), (33, 66000, 500, 16)])
-@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-def test_bf16_wsff_equals_ws(pmm, m, n, d, k, metric, monkeypatch):
-    rs = np.random.RandomState(m + n + d + k + 17)
-    q = rs.randn(m, d).astype(np.float32)
-    c = rs.randn(n, d).astype(np.float32)
-    c[n // 2:n // 2 + 20] = c[:20]  # exact ties across the corpus
-    q[m // 2] = 0.0                  # a zero-norm query row
-    (fi, fsc), (wi, wsc) = _ws_and_ff(q, c, k, metric, monkeypatch, var="PMM_BF16_WSFF")
-    assert np.array_equal(fi, wi)
-    assert np.array_equal(fsc.view(np.uint32), wsc.view(np.uint32))
-
-
-@pytest.mark.parametrize("knobs", [{}, {"PMM_WSFF_J": "1"}, {"PMM_FF_CAP": "64"}, {"PMM_WSFF_J": "1", "PMM_FF_CAP": "64"}])
-@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-def test_bf16_wsff_forced_and_reruns_equal_ws(pmm, knobs, metric, monkeypatch):
-    # forced where the guess is poor (PMM_BF16_WSFF=2), the sample's best as
-    # the guess (j = 1: fewer than k survivors in many rows) and regions far
-    # too small (dropped items): the affected rows are re-run; every list
-    # still equals the default mode's, bit for bit
-    rs = np.random.RandomState(91 + len(knobs) + METRICS[metric])
-    m, n, d, k = 400, 70000, 256, 60
-    q = rs.randn(m, d).astype(np.float32)
-    c = rs.randn(n, d).astype(np.float32)
-    for kk, v in knobs.items():
-        monkeypatch.setenv(kk, v)
-    monkeypatch.setenv("PMM_BF16_WSFF", "2")
-    fi, fsc = gpu_topk_bf16(q, c, k, metric)
-    for kk in knobs:
-        monkeypatch.delenv(kk)
-    monkeypatch.setenv("PMM_BF16_WSFF", "0")
-    wi, wsc = gpu_topk_bf16(q, c, k, metric)
-    assert np.array_equal(fi, wi)
-    assert np.array_equal(fsc.view(np.uint32), wsc.view(np.uint32))
-
-
-def test_bf16_wsff_device_api_300k_rows_equal_ws(pmm, monkeypatch):
-    import torch
-
-    n = _native()
-    dev = torch.device("cuda:0")
-    g = torch.Generator(device=dev)
-    g.manual_seed(41)
-    m, N, d, k = 3000, 300000, 768, 100
-    q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
-    c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
-    outs = []
-    for v in ("1", "0"):
-        monkeypatch.setenv("PMM_BF16_WSFF", v)
-        oi = torch.empty((m, k), dtype=torch.int32, device=dev)
-        osc = torch.empty((m, k), dtype=torch.float32, device=dev)
-        n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS["euclidean"],
-                           oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        outs.append((oi.cpu().numpy(), osc.cpu().numpy()))
-    assert np.array_equal(outs[0][0], outs[1][0])
-    assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
 
 
 @pytest.mark.parametrize("m,n,d,k", [(300, 70000, 256, 10), (520, 200000, 768, 100), (257, 131072, 384, 32),
