@@ -5,7 +5,7 @@ out=$1; to=$2; shift 2
 for i in $(seq 1 15); do
   /usr/local/graft/bin/gpurun --timeout $to -- "$@" > $out 2>&1
   rc=$?
-  if grep -q "no free box\|stopped responding while being prepared\|backing off\|taken away" $out && ! grep -q "status=ok\|status=fail" $out; then sleep 100; continue; fi
+  if grep -q "no free box\|stopped responding while being prepared\|backing off\|taken away\|slot(s) on this pod are busy" $out && ! grep -q "status=ok\|status=fail" $out; then sleep 100; continue; fi
   exit $rc
 done
 exit $rc
