@@ -100,6 +100,32 @@ __device__ __forceinline__ void f64_tile(const double *__restrict__ q, int64_t l
   }
 }
 
+// Tile order of the 1-D grid (both kernels below).  Consecutive workgroups
+// go to the 8 XCDs in turn, and each XCD has its own L2, so workgroup b works
+// on logical tile x * ceil(T / 8) + b / 8 (x = b % 8): every XCD walks a
+// contiguous stretch of the logical order, which takes the row blocks in
+// groups of kF64GroupRows (row block fastest inside a group, then the column
+// block): the ~128 workgroups an XCD holds at once share 8 row tiles and ~16
+// column tiles, 3 MB at D = 256, instead of streaming every corpus tile once
+// per row block (a column-block-fastest 2-D grid re-read the corpus from HBM
+// M / 64 times).
+constexpr int kF64GroupRows = 8;
+__device__ __forceinline__ bool f64_tile_of(int nR, int nC, int &r, int &c) {
+  const int64_t T = (int64_t)nR * nC;
+  const int64_t per = (T + 7) / 8;
+  const int64_t L = (int64_t)(blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (L >= T) return false;
+  const int64_t span = (int64_t)kF64GroupRows * nC;
+  const int64_t g = L / span, w = L - g * span;
+  const int gr = (int)min<int64_t>(kF64GroupRows, nR - g * kF64GroupRows);  // rows in this group
+  r = (int)(g * kF64GroupRows + w % gr);
+  c = (int)(w / gr);
+  return true;
+}
+__host__ static inline unsigned f64_grid(int nR, int nC) {
+  return (unsigned)(((int64_t)nR * nC + 7) / 8 * 8);
+}
+
 // Store mode (`.pmm.matmul` f64, src/metrics.rs:40-157; and the materialised
 // top-k path's transformed scores, :258-311).
 template <int METRIC, int XF>
@@ -111,7 +137,9 @@ __global__ __launch_bounds__(256) void gemm_f64_store_kernel(const double *__res
   __shared__ double lds[2 * 2 * kF64LdsBuf];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  int rb, cbk;
+  if (!f64_tile_of((M + 63) / 64, (N + 63) / 64, rb, cbk)) return;
+  const int r0 = rb * 64, c0 = cbk * 64;
   f64x4 acc[2][2];
   f64_tile(q + (int64_t)r0 * ldq, ldq, M - r0, c + (int64_t)c0 * ldc, ldc, N - c0, D, acc, lds);
   const int row0 = r0 + (wid >> 1) * 32, col0 = c0 + (wid & 1) * 32;
@@ -135,7 +163,7 @@ hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, 
                                  int metric, int store_metric, double *out, int64_t ldo,
                                  hipStream_t s) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  const dim3 grid((N + 63) / 64, (M + 63) / 64), blk(256);
+  const dim3 grid(f64_grid((M + 63) / 64, (N + 63) / 64)), blk(256);
   if (!store_metric || metric == kMetricDot)
     gemm_f64_store_kernel<kMetricDot, 0><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
   else if (metric == kMetricCosine)
@@ -156,7 +184,9 @@ __global__ __launch_bounds__(256) void gemm_f64_topk_kernel(F64TopkArgs a) {
   __shared__ double lds[2 * 2 * kF64LdsBuf];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
-  const int r0 = blockIdx.y * 64, lc0w = blockIdx.x * 64;  // lc: column within the chunk
+  int rb, cbk;
+  if (!f64_tile_of((a.M + 63) / 64, (a.ncol + 63) / 64, rb, cbk)) return;
+  const int r0 = rb * 64, lc0w = cbk * 64;  // lc: column within the chunk
   f64x4 acc[2][2];
   f64_tile(a.q + (int64_t)r0 * a.ldq, a.ldq, a.M - r0, a.c + (int64_t)(a.col0 + lc0w) * a.ldc, a.ldc,
            a.ncol - lc0w, a.D, acc, lds);
@@ -250,7 +280,7 @@ __global__ __launch_bounds__(256) void gemm_f64_topk_kernel(F64TopkArgs a) {
 
 hipError_t launch_gemm_f64_topk(const F64TopkArgs &a, hipStream_t s) {
   if (a.M <= 0 || a.ncol <= 0) return hipSuccess;
-  const dim3 grid((a.ncol + 63) / 64, (a.M + 63) / 64), blk(256);
+  const dim3 grid(f64_grid((a.M + 63) / 64, (a.ncol + 63) / 64)), blk(256);
   if (a.metric == kMetricCosine) gemm_f64_topk_kernel<kMetricCosine><<<grid, blk, 0, s>>>(a);
   else if (a.metric == kMetricEuclidean) gemm_f64_topk_kernel<kMetricEuclidean><<<grid, blk, 0, s>>>(a);
   else gemm_f64_topk_kernel<kMetricDot><<<grid, blk, 0, s>>>(a);
