@@ -667,7 +667,14 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
     int64_t ns = std::min<int64_t>(n, next_pow2((int)std::max<int64_t>(256, 8 * k), 256));
     if (const char *ne = getenv("PMM_SEED_NS")) ns = std::min<int64_t>(n, std::max<int64_t>(atoll(ne), k));
     const char *se = getenv("PMM_SEED");
-    bool seed = (se ? atoi(se) != 0 : ((int64_t)p.tps * gemm_f32_bn(p.variant) < 8192 && n >= 4 * ns)) &&
+    // (only when most query blocks run as split units: a block run whole
+    // carries its threshold across the corpus and gains nothing from the
+    // seed, which costs m * ns * d fmaf on the vector units -- at a c3 shard
+    // of 8, 100k x 125k x 768 with 256 of 391 blocks whole, 9.3 ms for no
+    // GEMM time saved; tools/experiments/shard_shapes.py, profiles/r4_shards/)
+    const bool mostly_split = 2 * (int64_t)p.qb_full < (int64_t)p.QB;
+    bool seed = (se ? atoi(se) != 0
+                    : ((int64_t)p.tps * gemm_f32_bn(p.variant) < 8192 && n >= 4 * ns && mostly_split)) &&
                 ns >= k && ns < n && ns <= kSeedMaxNs && !keep_gthr &&
                 (size_t)m * ns * 4 <= p.off_qn - p.off_cand;
     FusedF32 f{q, ldq, m, c, ldc, n, dp, k, metric, qn, cn, cn + n};
