@@ -48,6 +48,8 @@ struct GemmF32Args {
   unsigned *cnt;                  // [M*S] candidate counts
   unsigned long long *gthr;       // [M] shared per-row threshold, zeroed per call
   unsigned long long *wq;         // per-wave survivor queue [grid][NW][32 * BN]
+  int qcap;                       // f32 kernel: survivor-queue entries per wave in LDS
+                                  // (set by launch_gemm_f32; past them, wq)
   float *out;                     // store mode: out[M][ldo]
   int64_t ldo;
   int store_metric;               // store mode: 1 = metric-transformed score, 0 = raw dot

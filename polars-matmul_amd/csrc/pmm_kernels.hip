@@ -82,20 +82,37 @@ hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld
 #define PMM_F32_DEFER 1
 #endif
 
-template <int NB, int NW>
+// The K-step ring is double-buffered.  (A deeper ring for the small
+// variants -- step g + NS - 1 issued from asm behind step g, counted vmcnt
+// waits -- measured slower at c1 with 3-5 stages: 0.080 vs 0.074 ms per
+// fused launch, profiles/r4_c1/deep_ring_ab.txt; round 3 found the same for
+// 128 x 128.  The loop does not wait on the corpus stream.)
+constexpr int kF32Stages = 2;
+
+// AK (query rows resident): the unit's query block stays in LDS for all its
+// K steps (loaded once at unit start, after the carve below), and the ring
+// stages hold corpus pieces only -- every tile after the first re-streamed
+// the block from L2 (two thirds of a 128 x 64 tile's DMA at D = 256).
+template <int NB, int NW, bool AK = false>
 struct GemmShape {
+  static constexpr int NS = kF32Stages;
   static constexpr int BN = 32 * NB;                // corpus columns per tile
   static constexpr int BM = 32 * NW;                // query rows per workgroup
   static constexpr int A_BYTES = NW * 4096;         // NW waves x 32 rows x 128 B
   static constexpr int B_BYTES = BN * 128;          // BN rows x 128 B
-  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int A_IN_STAGE = AK ? 0 : A_BYTES;
+  static constexpr int STAGE = A_IN_STAGE + B_BYTES;
   static constexpr int BPIECES = B_BYTES / 1024 / NW;  // 1 KiB LDS-DMA pieces per wave
-  static constexpr int OFF_THR = 2 * STAGE;
+  static constexpr int OFF_THR = NS * STAGE;
   static constexpr int OFF_CNT = OFF_THR + BM * 8;
   static constexpr int OFF_QEX = OFF_CNT + BM * 4;   // exact row norm (epilogue)
   static constexpr int OFF_LO = OFF_QEX + BM * 4;    // pre-filter bound per row
-  static constexpr int OFF_CV = OFF_LO + BM * 4;     // column factors, 2 tiles
-  static constexpr int OFF_UNIT = OFF_CV + 2 * BN * 4;
+  static constexpr int OFF_CV = OFF_LO + BM * 4;     // column factors, NS tiles
+  // column norms of the exact re-scores, NS tiles: the small variants only
+  // (the 256 x 256 one's carve has no room left at k = 100)
+  static constexpr bool CNL = NB <= 4 && NW == 4;
+  static constexpr int OFF_CN = OFF_CV + NS * BN * 4;
+  static constexpr int OFF_UNIT = OFF_CN + (CNL ? NS * BN * 4 : 0);
   static constexpr int OFF_SCR = OFF_UNIT + 16;
   static_assert(B_BYTES % (1024 * NW) == 0, "corpus tile must split into 1 KiB pieces per wave");
   static_assert(OFF_SCR % 16 == 0, "LDS carve must stay 16-byte aligned");
@@ -112,12 +129,18 @@ constexpr int kVarNW[kGemmVariants] = {4, 4, 8, 8, 4};
 int gemm_f32_bm(int variant) { return 32 * kVarNW[variant]; }
 int gemm_f32_bn(int variant) { return 32 * kVarNB[variant]; }
 
-size_t gemm_f32_lds_bytes(int variant, int mode, int capg) {
+// bytes at ns LDS stages; the fit checks use the double-buffered carve
+// (ks_resident > 0: the AK carve, query rows of ks_resident K steps after it)
+static size_t gemm_f32_lds_bytes_ak(int variant, int mode, int capg, int ks_resident) {
+  const int ns = kF32Stages;
   const int nb = kVarNB[variant], nw = kVarNW[variant];
-  const size_t stage = (size_t)nw * 4096 + (size_t)32 * nb * 128;
-  const size_t fixed = 2 * stage + (size_t)32 * nw * 20 + (size_t)2 * 32 * nb * 4 + 16;
-  return fixed + (mode == 0 ? (size_t)nw * capg * 8 : 0);
+  const size_t a_bytes = (size_t)nw * 4096;
+  const size_t stage = (ks_resident ? 0 : a_bytes) + (size_t)32 * nb * 128;
+  const bool cnl = nb <= 4 && nw == 4;  // GemmShape::CNL
+  const size_t fixed = ns * stage + (size_t)32 * nw * 20 + (size_t)(cnl ? 2 : 1) * ns * 32 * nb * 4 + 16;
+  return fixed + (mode == 0 ? (size_t)nw * capg * 8 : 0) + (size_t)ks_resident * a_bytes;
 }
+size_t gemm_f32_lds_bytes(int variant, int mode, int capg) { return gemm_f32_lds_bytes_ak(variant, mode, capg, 0); }
 
 
 // K order of the f32 MFMA chain (A/B builds: -DPMM_F32_KORDER=n):
@@ -144,15 +167,17 @@ size_t gemm_f32_lds_bytes(int variant, int mode, int capg) {
 #define PMM_F32_KORDER_SMALL 3
 #endif
 
-template <int NB, int NW, int MODE, int METRIC>
+template <int NB, int NW, int MODE, int METRIC, bool AK>
 __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a) {
-  using G = GemmShape<NB, NW>;
+  using G = GemmShape<NB, NW, AK>;
+  constexpr int NS = G::NS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   u64 *thr_l = (u64 *)(smem + G::OFF_THR);
   unsigned *cnt_l = (unsigned *)(smem + G::OFF_CNT);
   float *qex_l = (float *)(smem + G::OFF_QEX);
   float *lo_l = (float *)(smem + G::OFF_LO);
   float *cv_l = (float *)(smem + G::OFF_CV);
+  float *cn_l = (float *)(smem + G::OFF_CN);
   int *unit_l = (int *)(smem + G::OFF_UNIT);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -160,6 +185,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   const int r32 = lane & 31, h = lane >> 5;
   const int KS = a.D >> 5;
   u64 *scr = (u64 *)(smem + G::OFF_SCR) + (size_t)wid * a.capg;
+  // AK: the resident query rows, [KS][NW waves][32 rows x 128 B]
+  char *a_res = smem + G::OFF_SCR + (MODE == 0 ? (size_t)NW * a.capg * 8 : 0);
+  // the survivor queue's first a.qcap entries per wave (the rest: a.wq)
+  u64 *lq = (u64 *)(a_res + (AK ? (size_t)KS * G::A_BYTES : 0)) + (size_t)wid * a.qcap;
   u64 *thr_w = thr_l + wid * 32;
   unsigned *cnt_w = cnt_l + wid * 32;
   float *qex_w = qex_l + wid * 32;  // per-row constants live in LDS, not in VGPRs
@@ -208,7 +237,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   // Per-lane LDS read offsets (within a stage).
   const int swz = (r32 >> 1) & 7;
   const int a_rd = wid * 4096 + r32 * 128;
-  const int b_rd = G::A_BYTES + r32 * 128;
+  const int b_rd = G::A_IN_STAGE + r32 * 128;
 
   int buf = 0;
   for (;;) {
@@ -268,29 +297,40 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         if (dw == 4) __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (LDS_AS void *)dst, 4, voff, soff, 0, 0);
         else dma16(r, dst, voff, soff);
       };
+      // (ablation build, PMM_ABLATE=3 / 4: the query rows load only in the
+      // unit's first tile -- later tiles read stale rows, results wrong)
+      const bool skip_a = (PMM_ABL(a.ablate) == 3 || PMM_ABL(a.ablate) == 4) && tile != t0;
+      constexpr int AS = AK ? 0 : AP;  // A pieces per step in the ring
 #pragma unroll
-      for (int i = 0; i < AP; i++)
-        if (i >= lo && i < hi) dma(ra, st + wid * 4096 + i * APIECE, a_voff[i], ADW);
+      for (int i = 0; i < AS; i++)
+        if (i >= lo && i < hi && !skip_a) dma(ra, st + wid * 4096 + i * APIECE, a_voff[i], ADW);
 #pragma unroll
       for (int i = 0; i < BP; i++)
-        if (AP + i >= lo && AP + i < hi) dma(rb, st + G::A_BYTES + (i * NW + wid) * BPIECE, b_voff[i], BDW);
+        if (AS + i >= lo && AS + i < hi) dma(rb, st + G::A_IN_STAGE + (i * NW + wid) * BPIECE, b_voff[i], BDW);
       if (MODE == 0 && XFORM && ks == 0 && wid == 0 && lo == 0) {
         // the tile's pre-filter column factors ride with its first K step
         const int col0 = tile * G::BN;
         const __amdgpu_buffer_rsrc_t rc =
             make_rsrc(a.cpre + col0, (int64_t)min(G::BN, a.N - col0) * 4);
-        char *dst = (char *)(cv_l + (tile & 1) * G::BN);
+        // (and, small variants, the column norms of its exact re-scores)
+        const __amdgpu_buffer_rsrc_t rn = make_rsrc(a.cn + col0, (int64_t)min(G::BN, a.N - col0) * 4);
+        char *dst = (char *)(cv_l + ((unsigned)tile % NS) * G::BN);
+        char *dsn = (char *)(cn_l + ((unsigned)tile % NS) * G::BN);
 #pragma unroll
-        for (int i = 0; i < G::BN / 64; i++)
+        for (int i = 0; i < G::BN / 64; i++) {
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rc, (LDS_AS void *)(dst + i * 256), 4,
                                                    (uint32_t)(lane * 4 + i * 256), 0, 0, 0);
+          if (G::CNL)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(rn, (LDS_AS void *)(dsn + i * 256), 4,
+                                                     (uint32_t)(lane * 4 + i * 256), 0, 0, 0);
+        }
       }
     };
 
     // the next K step's DMA goes out behind MFMA groups 0 .. NPART-1 of this
     // one, TP / NPART pieces each (the natural-order image takes 4x the
     // pieces of the 16-byte form; spread, they do not stall one group)
-    constexpr int TP = AP + BP;
+    constexpr int TP = (AK ? 0 : AP) + BP;
 #ifndef PMM_F32_DMA_PARTS
 #define PMM_F32_DMA_PARTS 1  // (A/B at c3: 4 measured 7% slower, 2 1.1% slower)
 #endif
@@ -312,6 +352,19 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     // profiles/r3_c1/block_prefilter_ab.txt)
     static_assert(TP % NPART == 0 && NPART <= 4, "DMA pieces split evenly over the MFMA groups");
     __amdgpu_buffer_rsrc_t rb = rsrc_b(t0);
+    if (AK) {
+      // the unit's query rows, every K step, once (the unit-start barriers
+      // above: every wave is done with the previous unit's rows)
+      for (int ks = 0; ks < KS; ks++)
+#pragma unroll
+        for (int i = 0; i < AP; i++) {
+          char *dst = a_res + ks * G::A_BYTES + wid * 4096 + i * APIECE;
+          if (ADW == 4)
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void *)dst, 4, a_voff[i], (uint32_t)ks * 128u, 0, 0);
+          else
+            dma16(ra, dst, a_voff[i], (uint32_t)ks * 128u);
+        }
+    }
     stage(buf, rb, 0, t0, 0, TP);
     for (int tile = t0; tile < t1; tile++) {
       const bool last_tile = (tile + 1) >= t1;
@@ -341,7 +394,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         // {0,2,1,3} = k pairs (8qd,+1) (8qd+2,+3) (8qd+4,+5) (8qd+6,+7).
         auto rd_frag = [&](int qd, f32x4 &av, f32x4 (&b)[NB]) __attribute__((always_inline)) {
           const int co = KO == 0 ? 16 * ((4 * h + qd) ^ swz) : 16 * ((2 * qd + h) ^ swz);
-          av = *(const f32x4 *)(st + a_rd + co);
+          av = *(const f32x4 *)((AK ? a_res + ks * G::A_BYTES : st) + a_rd + co);
 #pragma unroll
           for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
         };
@@ -400,12 +453,15 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             // matrix pipe restarts right after the barrier
             __builtin_amdgcn_sched_barrier(0);
             constexpr int PER = TP / NPART;
-            if (ks + 1 < KS) stage(buf ^ 1, rb, ks + 1, tile, qd * PER, qd * PER + PER);
-            else if (!last_tile) stage(buf ^ 1, rbn, 0, tile + 1, qd * PER, qd * PER + PER);
+            if (ks + 1 < KS) {
+              stage(buf ^ 1, rb, ks + 1, tile, qd * PER, qd * PER + PER);
+            } else if (!last_tile) {
+              stage(buf ^ 1, rbn, 0, tile + 1, qd * PER, qd * PER + PER);
+            }
             __builtin_amdgcn_sched_barrier(0);
           }
         }
-        buf ^= 1;
+        buf = buf + 1 == NS ? 0 : buf + 1;
       };
       using Yes = std::integral_constant<bool, true>;
       using No = std::integral_constant<bool, false>;
@@ -419,7 +475,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       rb = rbn;
 
       const int col0 = tile * G::BN;
-      if (PMM_ABL(a.ablate) == 1) {
+      if (PMM_ABL(a.ablate) == 1 || PMM_ABL(a.ablate) == 4) {
         // ablation build path: keep the accumulators live, skip the epilogue
         float sink = 0.0f;
 #pragma unroll
@@ -462,7 +518,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         // (one per lane), and append to the rows' candidate buffers.  The
         // queue lives in global memory (L2): a tile can produce up to
         // 32 x BN survivors per wave (a unit's first tile).
-        const float *cvt = cv_l + (tile & 1) * G::BN;
+        const float *cvt = cv_l + ((unsigned)tile % NS) * G::BN;
+        const float *cnt_t = cn_l + ((unsigned)tile % NS) * G::BN;
         u64 *gq = a.wq + ((size_t)blockIdx.x * NW + wid) * (size_t)(32 * G::BN);
         int qlen = 0;  // wave-uniform
         // queue item high word = row-in-wave | col-in-tile << 5 = lane part +
@@ -491,24 +548,31 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             if (m == 0ull) continue;
             if (p && PMM_ABL(a.ablate) != 2) {
               const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
-              gq[qlen + lanes_below(m)] = (u64)__float_as_uint(v) | ((u64)hi << 32);
+              const int qi = qlen + lanes_below(m);
+              const u64 item = (u64)__float_as_uint(v) | ((u64)hi << 32);
+              if (qi < a.qcap) lq[qi] = item;
+              else gq[qi] = item;
             }
             qlen += __popcll(m);
           }
         }
         if (PMM_ABL(a.ablate) == 2) qlen = 0;  // ablation: pre-filter only
         if (qlen) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // queue stores reached L2
+          // queue entries past the LDS part: their stores reached L2
+          if (qlen > a.qcap) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          wave_sync();  // every lane's LDS queue entries written
           for (int base = 0; base < qlen; base += 64) {
             const int i = base + lane;
             if (i < qlen) {
-              // sc1 load: bypasses this CU's L1, reads what the stores left in L2
-              const u64 it = __hip_atomic_load(gq + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              // (global part: an sc1 load bypasses this CU's L1, reads what
+              // the stores left in L2)
+              const u64 it = i < a.qcap ? lq[i] : __hip_atomic_load(gq + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               const float v = __uint_as_float((uint32_t)it);
               const int rl = (int)((it >> 32) & 31u);
-              const int gcol = col0 + (int)(it >> 37);
+              const int tc = (int)(it >> 37);
+              const int gcol = col0 + tc;
               const float sc =
-                  exact_score<METRIC>(v, XFORM ? qex_w[rl] : 0.0f, XFORM ? a.cn[gcol] : 0.0f);
+                  exact_score<METRIC>(v, XFORM ? qex_w[rl] : 0.0f, XFORM ? (G::CNL ? cnt_t[tc] : a.cn[gcol]) : 0.0f);
               const uint32_t key = okey32(METRIC == kMetricEuclidean ? -sc : sc);
               const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
               if (comp > thr_w[rl]) {
@@ -544,42 +608,66 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   }
 }
 
-template <int NB, int NW, int MODE, int METRIC>
-static hipError_t launch_gemm_f32_t(const GemmF32Args &a, int grid, size_t lds, hipStream_t s) {
+// (top-k mode: the survivor queue's LDS part takes what the carve leaves of
+// the CU's 160 KiB, up to a tile's 32 x BN entries per wave, in 64-entry
+// steps; PMM_F32_QCAP=0: the global queue only, for A/B runs)
+template <int NB, int NW, int MODE, int METRIC, bool AK>
+static hipError_t launch_gemm_f32_t(const GemmF32Args &a_in, int grid, size_t lds, hipStream_t s) {
+  GemmF32Args a = a_in;
+  a.qcap = 0;
+  static const bool lq_on = !(getenv("PMM_F32_QCAP") && atoi(getenv("PMM_F32_QCAP")) == 0);
+  if (MODE == 0 && lq_on && lds < 160 * 1024) {
+    const size_t per = (160 * 1024 - lds) / (NW * 8);
+    a.qcap = (int)(std::min<size_t>(per, 32 * 32 * NB) / 64 * 64);
+    lds += (size_t)NW * a.qcap * 8;
+  }
   static bool attr_set = false;  // opt in to > 64 KiB dynamic LDS
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void *)gemm_f32_kernel<NB, NW, MODE, METRIC>,
+    hipError_t e = hipFuncSetAttribute((const void *)gemm_f32_kernel<NB, NW, MODE, METRIC, AK>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  gemm_f32_kernel<NB, NW, MODE, METRIC><<<dim3(grid), dim3(NW * 64), lds, s>>>(a);
+  gemm_f32_kernel<NB, NW, MODE, METRIC, AK><<<dim3(grid), dim3(NW * 64), lds, s>>>(a);
   return hipGetLastError();
 }
 
-template <int NB, int NW>
-static hipError_t launch_gemm_f32_v(const GemmF32Args &a, int mode, int grid, size_t lds,
-                                    hipStream_t s) {
+template <int NB, int NW, bool AK = false>
+static hipError_t launch_gemm_f32_v(const GemmF32Args &a, int mode, int grid, size_t lds, hipStream_t s) {
   if (mode == 0) {
-    if (a.metric == kMetricCosine) return launch_gemm_f32_t<NB, NW, 0, kMetricCosine>(a, grid, lds, s);
-    if (a.metric == kMetricDot) return launch_gemm_f32_t<NB, NW, 0, kMetricDot>(a, grid, lds, s);
-    return launch_gemm_f32_t<NB, NW, 0, kMetricEuclidean>(a, grid, lds, s);
+    if (a.metric == kMetricCosine) return launch_gemm_f32_t<NB, NW, 0, kMetricCosine, AK>(a, grid, lds, s);
+    if (a.metric == kMetricDot) return launch_gemm_f32_t<NB, NW, 0, kMetricDot, AK>(a, grid, lds, s);
+    return launch_gemm_f32_t<NB, NW, 0, kMetricEuclidean, AK>(a, grid, lds, s);
   }
   if (!a.store_metric || a.metric == kMetricDot)
-    return launch_gemm_f32_t<NB, NW, 1, kMetricDot>(a, grid, lds, s);
-  if (a.metric == kMetricCosine) return launch_gemm_f32_t<NB, NW, 1, kMetricCosine>(a, grid, lds, s);
-  return launch_gemm_f32_t<NB, NW, 1, kMetricEuclidean>(a, grid, lds, s);
+    return launch_gemm_f32_t<NB, NW, 1, kMetricDot, AK>(a, grid, lds, s);
+  if (a.metric == kMetricCosine) return launch_gemm_f32_t<NB, NW, 1, kMetricCosine, AK>(a, grid, lds, s);
+  return launch_gemm_f32_t<NB, NW, 1, kMetricEuclidean, AK>(a, grid, lds, s);
+}
+
+// Small variants: resident query rows (PMM_F32_AK, default on) when the unit
+// spans more than one tile and the carve fits (c1: 128 rows x D 256 = 128 KiB
+// of the 160), else the rows re-stream with every tile.
+#ifndef PMM_F32_AK
+#define PMM_F32_AK 1
+#endif
+template <int NB, int NW>
+static hipError_t launch_gemm_f32_small(const GemmF32Args &a, int variant, int mode, int grid, hipStream_t s) {
+  const size_t ak = gemm_f32_lds_bytes_ak(variant, mode, a.capg, a.D >> 5);
+  static const int ak_env = getenv("PMM_F32_AK") ? atoi(getenv("PMM_F32_AK")) : PMM_F32_AK;
+  if (ak_env && a.tps > 1 && ak <= 160 * 1024) return launch_gemm_f32_v<NB, NW, true>(a, mode, grid, ak, s);
+  return launch_gemm_f32_v<NB, NW>(a, mode, grid, gemm_f32_lds_bytes(variant, mode, a.capg), s);
 }
 
 hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid, hipStream_t s) {
   const size_t lds = gemm_f32_lds_bytes(variant, mode, a.capg);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   switch (variant) {
-    case 0: return launch_gemm_f32_v<4, 4>(a, mode, grid, lds, s);
+    case 0: return launch_gemm_f32_small<4, 4>(a, variant, mode, grid, s);
     case 1: return launch_gemm_f32_v<8, 4>(a, mode, grid, lds, s);
     case 2: return launch_gemm_f32_v<4, 8>(a, mode, grid, lds, s);
     case 3: return launch_gemm_f32_v<8, 8>(a, mode, grid, lds, s);
-    case 4: return launch_gemm_f32_v<2, 4>(a, mode, grid, lds, s);
+    case 4: return launch_gemm_f32_small<2, 4>(a, variant, mode, grid, s);
     default: return hipErrorInvalidValue;
   }
 }
