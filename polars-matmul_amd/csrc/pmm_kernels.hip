@@ -108,8 +108,9 @@ struct GemmShape {
   static constexpr int OFF_QEX = OFF_CNT + BM * 4;   // exact row norm (epilogue)
   static constexpr int OFF_LO = OFF_QEX + BM * 4;    // pre-filter bound per row
   static constexpr int OFF_CV = OFF_LO + BM * 4;     // column factors, NS tiles
-  // column norms of the exact re-scores, NS tiles: the small variants only
-  // (the 256 x 256 one's carve has no room left at k = 100)
+  // column norms of the exact re-scores, NS tiles, and the survivor queue in
+  // LDS: the small variants only (the 256 x 256 one's carve has no room left
+  // at k = 100; its survivors are rare after a unit's first tiles)
   static constexpr bool CNL = NB <= 4 && NW == 4;
   static constexpr int OFF_CN = OFF_CV + NS * BN * 4;
   static constexpr int OFF_UNIT = OFF_CN + (CNL ? NS * BN * 4 : 0);
@@ -550,7 +551,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
               const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
               const int qi = qlen + lanes_below(m);
               const u64 item = (u64)__float_as_uint(v) | ((u64)hi << 32);
-              if (qi < a.qcap) lq[qi] = item;
+              if (G::CNL && qi < a.qcap) lq[qi] = item;
               else gq[qi] = item;
             }
             qlen += __popcll(m);
@@ -559,14 +560,15 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         if (PMM_ABL(a.ablate) == 2) qlen = 0;  // ablation: pre-filter only
         if (qlen) {
           // queue entries past the LDS part: their stores reached L2
-          if (qlen > a.qcap) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          wave_sync();  // every lane's LDS queue entries written
+          if (!G::CNL || qlen > a.qcap) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (G::CNL) wave_sync();  // every lane's LDS queue entries written
           for (int base = 0; base < qlen; base += 64) {
             const int i = base + lane;
             if (i < qlen) {
               // (global part: an sc1 load bypasses this CU's L1, reads what
               // the stores left in L2)
-              const u64 it = i < a.qcap ? lq[i] : __hip_atomic_load(gq + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              const u64 it = (G::CNL && i < a.qcap) ? lq[i]
+                                                    : __hip_atomic_load(gq + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
               const float v = __uint_as_float((uint32_t)it);
               const int rl = (int)((it >> 32) & 31u);
               const int tc = (int)(it >> 37);
@@ -616,7 +618,7 @@ static hipError_t launch_gemm_f32_t(const GemmF32Args &a_in, int grid, size_t ld
   GemmF32Args a = a_in;
   a.qcap = 0;
   static const bool lq_on = !(getenv("PMM_F32_QCAP") && atoi(getenv("PMM_F32_QCAP")) == 0);
-  if (MODE == 0 && lq_on && lds < 160 * 1024) {
+  if (MODE == 0 && GemmShape<NB, NW, AK>::CNL && lq_on && lds < 160 * 1024) {
     const size_t per = (160 * 1024 - lds) / (NW * 8);
     a.qcap = (int)(std::min<size_t>(per, 32 * 32 * NB) / 64 * 64);
     lds += (size_t)NW * a.qcap * 8;
