@@ -529,32 +529,70 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         uint32_t opaque0;
         asm volatile("v_mov_b32 %0, 0" : "=v"(opaque0));
         const uint32_t lane_hi = opaque0 + 4u * (uint32_t)h + ((uint32_t)r32 << 5);
+        auto prefilter = [&](float v, float cv) __attribute__((always_inline)) {
+          if (METRIC == kMetricDot) return v;
+          if (METRIC == kMetricCosine) return v * cv;
+          return fmaf(2.0f, v, -cv);
+        };
+        if (G::CNL) {
+          // small variants (16 NB <= 64 scores per lane): every score's flag
+          // first (VALU only), one wave prefix sum of the lanes' counts, then
+          // each lane appends its own survivors at consecutive slots.  (A
+          // ballot + branch + slot per score serialised the 16 NB compares
+          // on scalar round trips: ~7 us of the c1 kernel's 74.)  The queue
+          // order changes; the results do not (any order of appends keeps a
+          // row's buffer a superset of its top-k above the threshold).
+          u64 bits = 0ull;
 #pragma unroll
-        for (int c = 0; c < NB; c++) {
-          const int gcol = col0 + 32 * c + r32;
-          const bool cvalid = gcol < a.N;
-          const float cv = XFORM ? cvt[32 * c + r32] : 0.0f;
-          auto prefilter = [&](int e) __attribute__((always_inline)) {
-            const float v = acc[c][e];
-            if (METRIC == kMetricDot) return v;
-            if (METRIC == kMetricCosine) return v * cv;
-            return fmaf(2.0f, v, -cv);
-          };
+          for (int c = 0; c < NB; c++) {
+            const bool cvalid = col0 + 32 * c + r32 < a.N;
+            const float cv = XFORM ? cvt[32 * c + r32] : 0.0f;
 #pragma unroll
-          for (int e = 0; e < 16; e++) {
-            const float v = acc[c][e];
-            const float pv = prefilter(e);
-            const bool p = cvalid && !(pv < lo[e]);
-            const u64 m = __ballot(p);
-            if (m == 0ull) continue;
-            if (p && PMM_ABL(a.ablate) != 2) {
-              const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
-              const int qi = qlen + lanes_below(m);
-              const u64 item = (u64)__float_as_uint(v) | ((u64)hi << 32);
-              if (G::CNL && qi < a.qcap) lq[qi] = item;
-              else gq[qi] = item;
+            for (int e = 0; e < 16; e++)
+              if (cvalid && !(prefilter(acc[c][e], cv) < lo[e])) bits |= 1ull << (16 * c + e);
+          }
+          const int nl = __popcll(bits);  // <= 64: 7 bits
+          int excl = 0, tot = 0;
+#pragma unroll
+          for (int j = 0; j < 7; j++) {
+            const u64 m = __ballot((nl >> j) & 1);
+            excl += lanes_below(m) << j;
+            tot += __popcll(m) << j;
+          }
+          if (bits && PMM_ABL(a.ablate) != 2) {
+            int qi = qlen + excl;
+#pragma unroll
+            for (int c = 0; c < NB; c++)
+#pragma unroll
+              for (int e = 0; e < 16; e++)
+                if ((bits >> (16 * c + e)) & 1ull) {
+                  const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
+                  const u64 item = (u64)__float_as_uint(acc[c][e]) | ((u64)hi << 32);
+                  if (qi < a.qcap) lq[qi] = item;
+                  else gq[qi] = item;
+                  qi++;
+                }
+          }
+          qlen += tot;
+        } else {
+#pragma unroll
+          for (int c = 0; c < NB; c++) {
+            const int gcol = col0 + 32 * c + r32;
+            const bool cvalid = gcol < a.N;
+            const float cv = XFORM ? cvt[32 * c + r32] : 0.0f;
+#pragma unroll
+            for (int e = 0; e < 16; e++) {
+              const float v = acc[c][e];
+              const float pv = prefilter(v, cv);
+              const bool p = cvalid && !(pv < lo[e]);
+              const u64 m = __ballot(p);
+              if (m == 0ull) continue;
+              if (p && PMM_ABL(a.ablate) != 2) {
+                const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
+                gq[qlen + lanes_below(m)] = (u64)__float_as_uint(v) | ((u64)hi << 32);
+              }
+              qlen += __popcll(m);
             }
-            qlen += __popcll(m);
           }
         }
         if (PMM_ABL(a.ablate) == 2) qlen = 0;  // ablation: pre-filter only
