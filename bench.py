@@ -50,6 +50,9 @@ CONFIGS = {
     "c3": (100_000, 1_000_000, 768, 100, "cosine", "f32"),
     "c4": (100_000, 1_000_000, 768, 100, "cosine", "bf16"),
     "c5": (1_000_000, 10_000_000, 1024, 100, "cosine", "f32"),
+    # configs[4]'s per-GPU work on one GPU: all 1M queries against rank 0's
+    # shard of the 8-way row split (corpus rows [0, 1.25M) of c5's corpus)
+    "c5_rank": (1_000_000, 1_250_000, 1024, 100, "cosine", "f32"),
     "c2": (1_000, 10_000, 256, 10, "dot", "f32"),
     "c1": (1_000, 10_000, 256, 10, "cosine", "f32"),
 }
@@ -415,9 +418,10 @@ def e2e_topk_line(reps=5, warm=2):
     then explode + unnest), median of `reps` after `warm` warm-ups, as the
     reference times it.  Legs: List and Array (FixedSizeList) inputs, f32 and
     f64 (the reference's "Varying Dtype"); `cached` = repeated calls with the
-    same corpus column (the device corpus cache hits after the first call),
-    `first_call` = the cache cleared before each call (corpus uploaded and its
-    norms computed every time).  Per leg the median call's split: extract
+    same corpus column (the device corpus cache -- f32 or f64 rows -- hits
+    after the first call: only the queries are uploaded), `first_call` = the
+    cache cleared before each call (corpus uploaded and its norms computed
+    every time).  Per leg the median call's split: extract
     (Arrow -> contiguous matrices), h2d / kernels / d2h (HIP events of the
     library), device_other (host time in the C-ABI call outside the events'
     span: staging, launch, sync), assemble (f64 widening + Arrow List[Struct])
@@ -437,7 +441,7 @@ def e2e_topk_line(reps=5, warm=2):
         ch = np.random.randn(N, D).astype(dtype)
         for fixed in (False, True):
             qa, ca = _arrow_rows(qh, fixed), _arrow_rows(ch, fixed)
-            legs = ("cached", "first_call") if dtype == np.float32 else ("cached",)
+            legs = ("cached", "first_call")  # f32 and f64 corpora are both cached on the device
             for leg in legs:
                 def call():
                     if leg == "first_call":
@@ -746,6 +750,29 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8, stride=1)
             savg = ks["shard_merge"][0] / 1000.0
             reduction["shard_merge"] = {"bytes_per_launch": sbytes, "kernel_ms_avg": round(savg * 1000.0, 3),
                                         "achieved": round(sbytes / savg / 1e9, 1), "unit": "GB/s"}
+    small = None
+    if not bf16 and seed_ms and M * n_loc * D < 10**11:
+        # each small launch of a reference-size step against
+        # its own floor.  The prologue (seed + norms + fills, one launch):
+        # reads Q and C once, writes the norms / pre-filter factors and the
+        # seeded thresholds, and runs the sample's dot products (2 M ns D
+        # flops) and the norms (2 (M + N) D) on the vector ALUs.  The merge:
+        # merge_bytes (the split counts, surviving candidates, thresholds,
+        # the M x k output).  floor = max(bytes / HBM peak, flops / f32 peak).
+        ns = min(n_loc, 1 << max(8, (8 * k - 1).bit_length()))
+        pbytes = (M + n_loc) * D * 4 + (M + 2 * n_loc) * 4 + M * 8
+        pflops = 2.0 * M * ns * D + 2.0 * (M + n_loc) * D
+        small = {"prologue": {"kernel": "prologue_kernel (seed dots + norms + fills)", "us_avg": round(seed_ms * 1000.0, 2),
+                              "bytes": pbytes, "flops": pflops, "seed_rows": ns}}
+        if ks["merge"][0] and merge_bytes:
+            small["merge"] = {"kernel": "merge_kernel", "us_avg": round(ks["merge"][0] * 1000.0, 2), "bytes": merge_bytes,
+                              "flops": 0.0}
+        for v in small.values():
+            floor_s = max(v["bytes"] / (HBM_PEAK_GBS * 1e9), v["flops"] / (MFMA_PEAK_TFLOPS["f32"] * 1e12))
+            v["floor_us"] = round(floor_s * 1e6, 2)
+            v["gbs"] = round(v["bytes"] / (v["us_avg"] * 1e-6) / 1e9, 1)
+            v["frac_of_floor"] = round(floor_s * 1e6 / v["us_avg"], 3)
+        small["fused_us_avg"] = round(gemm_ms * 1000.0, 2) if gemm_ms else None
     lists = out_i.cpu().numpy() if (world == 1 or rank == 0) else None
     fields = {
         "config": {"workload": f"{M}x{N}x{D} {cdt} {metric} k={k} ({name})", "queries": M, "corpus": N,
@@ -755,6 +782,8 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8, stride=1)
         "ms_per_step": round(ms_step, 3), "steps": steps, "warmup": warmup,
         "roofline": roof, "reduction_roofline": reduction, "check": check,
     }
+    if small:
+        fields["small_kernels"] = small
     del runner, ws
     return fields, q, c, lists
 
@@ -1023,6 +1052,8 @@ def extra_line(name, steps, warmup, dev, args):
     M, N, D = CONFIGS[name][:3]
     small = M * N * D < 10**11  # sub-millisecond steps: time more of them
     st, wu = (max(steps, 200), max(warmup, 10)) if small else (steps, warmup)
+    if name == "c5_rank":
+        st, wu = 2, 1  # ~18 s per step: 1 warm-up + 2 timed steps keep the default run within minutes
     fields, q, c, lists = measure(name, st, wu, 0, 1, None, dev, check_rows=8, stride=args.timing_stride)
     ref = args.ref_lists.get(CONFIGS[name][:5])
     if CONFIGS[name][5] == "bf16" and ref is not None and fields["check"] is not None:
@@ -1068,6 +1099,94 @@ def extra_line(name, steps, warmup, dev, args):
     return fields
 
 
+def _brief(rec):
+    """value / ms per step / roofline fraction of one line (None-free)."""
+    out = {}
+    for key in ("value", "ms_per_step", "ms_per_call"):
+        if rec.get(key) is not None:
+            out[key] = rec[key]
+    roof = rec.get("roofline") or {}
+    if roof.get("frac") is not None:
+        out["frac"] = roof["frac"]
+    if roof.get("kernel_ms_avg") is not None:
+        out["kernel_ms"] = roof["kernel_ms_avg"]
+    return out
+
+
+def summary_of(line):
+    """A compact digest of the whole line (the headline and every extra's
+    value, ms per step and roofline fraction), printed as the line's LAST key
+    so that a reader of only the tail of stdout (the driver keeps the last
+    16 kB) sees every config's numbers."""
+    out = {"headline": dict(_brief(line), config=line["config"]["workload"])}
+    for name, rec in (line.get("extra") or {}).items():
+        if not isinstance(rec, dict):
+            continue
+        if name in ("c1_f64", "f64_large"):
+            b = _brief(rec.get("default") or {})
+            b["fused_ms"] = (rec.get("fused") or {}).get("ms_per_step")
+            b["materialised_ms"] = (rec.get("materialised") or {}).get("ms_per_step")
+            out[name] = b
+            continue
+        b = _brief(rec)
+        if name == "c1" and isinstance(rec.get("boundary"), dict):
+            b["e2e_ms"] = {leg: v["ms_per_call"] for leg, v in rec["boundary"].items()
+                           if isinstance(v, dict) and "ms_per_call" in v}
+            b["e2e_h2d_ms"] = {leg: v["split_ms"]["h2d"] for leg, v in rec["boundary"].items()
+                               if isinstance(v, dict) and "split_ms" in v}
+        if rec.get("reduction_roofline"):
+            b["merge_frac_hbm"] = rec["reduction_roofline"].get("frac")
+        if rec.get("small_kernels"):
+            b["small_kernels_us"] = {kk: (v.get("us_avg") if isinstance(v, dict) else v)
+                                     for kk, v in rec["small_kernels"].items()}
+        if rec.get("cpu_baseline"):
+            b["cpu_baseline"] = rec["cpu_baseline"].get("value")
+        out[name] = b
+    cpu = line.get("cpu_baseline")
+    if cpu:
+        out["cpu_baseline"] = {"value": cpu.get("value"), "unit": cpu.get("unit"), "cores": cpu.get("cores")}
+    return out
+
+
+def descendants(pid: int):
+    """Live descendant processes of pid (via /proc/<pid>/task/*/children)."""
+    out, todo = [], [pid]
+    while todo:
+        p = todo.pop()
+        try:
+            tasks = os.listdir(f"/proc/{p}/task")
+        except OSError:
+            continue
+        for t in tasks:
+            try:
+                with open(f"/proc/{p}/task/{t}/children") as f:
+                    kids = [int(x) for x in f.read().split()]
+            except (OSError, ValueError):
+                continue
+            for kid in kids:
+                try:
+                    with open(f"/proc/{kid}/cmdline", "rb") as f:
+                        cmd = f.read().replace(b"\0", b" ").decode(errors="replace").strip()
+                except OSError:
+                    cmd = "?"
+                out.append((kid, p, cmd))
+                todo.append(kid)
+    return out
+
+
+def report_descendants(tag: str) -> None:
+    """the driver saw one process alive at the end of the
+    bench (procs_at_end: 1) while an N = 1 run starts none on purpose; name
+    every descendant still alive (and this process's threads) on stderr."""
+    kids = descendants(os.getpid())
+    try:
+        nthreads = len(os.listdir(f"/proc/{os.getpid()}/task"))
+    except OSError:
+        nthreads = -1
+    log(f"[bench] {tag}: pid {os.getpid()}, {nthreads} threads, {len(kids)} live descendant process(es)"
+        + "".join(f"\n[bench]   pid {k} (parent {p}): {c[:200]}" for k, p, c in kids))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -1079,10 +1198,11 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="oracle baseline threads (0 = available_parallelism(), as faer's Rayon(0))")
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
-    ap.add_argument("--extra", default="c4,c1,c2,c1_f64,f64_large,matmul",
+    ap.add_argument("--extra", default="c4,c1,c2,c1_f64,f64_large,matmul,c5_rank",
                     help="comma-separated secondary configs measured after the main line (N=1; 'none' = none; "
                          "'matmul' = .pmm.matmul at the c1 size; 'c1_f64' = the f64 top-k at the c1 size; "
-                         "'f64_large' = the f64 top-k at 4096 x 1M x 256)")
+                         "'f64_large' = the f64 top-k at 4096 x 1M x 256; 'c5_rank' = configs[4]'s per-GPU "
+                         "share, 1M x 1.25M x 1024, 1 warm-up + 2 timed steps)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 top-k")
     ap.add_argument("--timing-stride", type=int, default=0,
                     help="record the per-kernel HIP events on every n-th timed step (0: every step of "
@@ -1234,11 +1354,13 @@ def main():
         "extra": extra if inproc is None else dict(extra or {}, inproc=inproc),
         "check": fields["check"],
     }
-    print(json.dumps(line), flush=True)
+    line["summary"] = summary_of(line)  # (last key: see summary_of)
     if spawner:
         spawner.close()
     if dist:
         dist.destroy_process_group()
+    report_descendants("before the result line")
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

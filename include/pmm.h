@@ -260,11 +260,23 @@ int pmm_merge_topk_strided_device(const uint32_t *idx, const float *score, int64
  * the padded rows in HBM and the norms of every metric (src/metrics.rs:368-393,
  * computed once at creation).  A handle may be used from several threads
  * concurrently; it is bound to the device current at creation, or sharded over
- * the device list (pmm_set_devices) in effect then.
+ * the device list (pmm_set_devices) in effect then.  Its row type is fixed at
+ * creation: an f32 handle serves pmm_topk_f32_corpus (the reference's f32
+ * branch, src/matmul.rs:429-448), an f64 handle pmm_topk_f64_corpus (the f64
+ * branch, src/matmul.rs:449-468 -- what Polars' default Float64 columns take).
  * ------------------------------------------------------------------------- */
 typedef struct pmm_corpus pmm_corpus;
 
+#define PMM_DTYPE_F32 0
+#define PMM_DTYPE_F64 1
+
 int pmm_corpus_create_f32(const float *c, int64_t n, int64_t d, pmm_corpus **out);
+/* An f64 corpus: rows kept in f64 (stride roundup(d, 16), zero-padded) with
+ * their f64 norms of both metrics, on ONE device (the device list's first
+ * entry when pmm_set_devices is in effect: f64 work is not sharded). */
+int pmm_corpus_create_f64(const double *c, int64_t n, int64_t d, pmm_corpus **out);
+/* PMM_DTYPE_F32 or PMM_DTYPE_F64. */
+int pmm_corpus_dtype(const pmm_corpus *corpus, int *dtype);
 int pmm_corpus_destroy(pmm_corpus *corpus);
 int pmm_corpus_info(const pmm_corpus *corpus, int64_t *n, int64_t *d, int *device);
 /* Number of device shards of a corpus handle (1, or the device list's length
@@ -275,6 +287,15 @@ int pmm_corpus_shards(const pmm_corpus *corpus, int *shards);
  * results out; 0 <= k <= n). */
 int pmm_topk_f32_corpus(const pmm_corpus *corpus, const float *q, int64_t m, int64_t k,
                         int metric, uint32_t *out_idx, float *out_score);
+
+/* pmm_topk_f64 against an f64 corpus handle (host queries in, host results
+ * out; 0 <= k <= n; any k: the fused scan for k <= 1024 and a large score
+ * matrix, else the materialised path, as pmm_topk_f64_device).  The results
+ * equal pmm_topk_f64's bit for bit: the handle's norms are the ones every
+ * call would compute, by the same kernel.  An f32 handle: PMM_ERR_ARG (and
+ * pmm_topk_f32_corpus refuses an f64 handle the same way). */
+int pmm_topk_f64_corpus(const pmm_corpus *corpus, const double *q, int64_t m, int64_t k,
+                        int metric, uint32_t *out_idx, double *out_score);
 
 /* Per-kernel timing on the launch stream (hipEvents around each launch).
  * enable=1 starts recording; pmm_timing_read returns the summed milliseconds

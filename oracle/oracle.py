@@ -10,7 +10,8 @@ Every function restates a reference function (paths into the reference tree):
 * ``metric_from_str``  -> src/metrics.rs:20-27
 * ``norms``            -> src/metrics.rs:368-393
 * ``similarity``       -> src/metrics.rs:258-365 (GEMM + epilogue)
-* ``select_topk``      -> src/topk.rs:6-75
+* ``select_topk``      -> src/topk.rs:6-75 (the checker's total order, or
+                          Rust's select_nth_unstable_by restated for timing)
 * ``topk``             -> src/matmul.rs:420-469 (k clipped to N, f32 scores widened to f64)
 * ``matmul``           -> src/metrics.rs:40-255 (dst = Q * C^T)
 * ``pair_scores``      -> the element S[i, idx[i, j]] of ``similarity`` (f32),
@@ -67,6 +68,8 @@ def lib():
         L.oracle_similarity_f64.argtypes = [vp, i64, vp, i64, i64, i32, vp, i32]
         L.oracle_select_topk_f32.argtypes = [vp, i64, i64, i64, i32, vp, vp]
         L.oracle_select_topk_f64.argtypes = [vp, i64, i64, i64, i32, vp, vp]
+        L.oracle_select_topk_rs_f32.argtypes = [vp, i64, i64, i64, i32, vp, vp]
+        L.oracle_select_topk_rs_f64.argtypes = [vp, i64, i64, i64, i32, vp, vp]
         L.oracle_topk_f32.argtypes = [vp, i64, vp, i64, i64, i64, i32, i32, vp, vp]
         L.oracle_topk_f32.restype = i64
         L.oracle_topk_f64.argtypes = [vp, i64, vp, i64, i64, i64, i32, i32, vp, vp]
@@ -118,12 +121,21 @@ def similarity(q: np.ndarray, c: np.ndarray, metric: int, nthreads: int = 0) -> 
     return out
 
 
-def select_topk(s: np.ndarray, k: int, higher_is_better: bool):
+def select_topk(s: np.ndarray, k: int, higher_is_better: bool, algo: str = "total"):
+    """Per-row top-k of a score matrix (src/topk.rs:6-75).  algo="total": the
+    checker's quickselect under the fixed total order (score, NaN last, lower
+    index); algo="rust": Rust's select_nth_unstable_by + stable sort_by
+    restated (pmm_oracle.c, the CPU baseline's select; equal scores in
+    whatever order that algorithm leaves them, as in the reference)."""
     s = np.ascontiguousarray(s)
     m, n = s.shape
     idx = np.zeros((m, k), dtype=np.uint32)
     sc = np.zeros((m, k), dtype=s.dtype)
-    fn = lib().oracle_select_topk_f32 if s.dtype == np.float32 else lib().oracle_select_topk_f64
+    L = lib()
+    if algo == "rust":
+        fn = L.oracle_select_topk_rs_f32 if s.dtype == np.float32 else L.oracle_select_topk_rs_f64
+    else:
+        fn = L.oracle_select_topk_f32 if s.dtype == np.float32 else L.oracle_select_topk_f64
     fn(_p(s), m, n, k, int(higher_is_better), _p(idx), _p(sc))
     return idx, sc
 
@@ -157,11 +169,13 @@ def pair_scores(q: np.ndarray, c: np.ndarray, idx: np.ndarray, metric: int, nthr
     return out
 
 
-def topk_blas(q: np.ndarray, c: np.ndarray, k: int, metric: int, nthreads: int = 0, timings: dict = None):
+def topk_blas(q: np.ndarray, c: np.ndarray, k: int, metric: int, nthreads: int = 0, timings: dict = None,
+              select: str = "rust"):
     """The reference's topk structure with a BLAS-class threaded GEMM (see the
-    module docstring).  Returns (idx uint32 [M,k'], scores float64 [M,k']);
-    `timings`, if given, receives the seconds of each phase (norms, gemm,
-    epilogue, select)."""
+    module docstring) and, by default, Rust's own select algorithm restated
+    (select_topk(algo="rust")).  Returns (idx uint32 [M,k'], scores float64
+    [M,k']); `timings`, if given, receives the seconds of each phase (norms,
+    gemm, epilogue, select)."""
     import time
 
     dt = np.float32 if (q.dtype == np.float32 and c.dtype == np.float32) else np.float64
@@ -189,7 +203,7 @@ def topk_blas(q: np.ndarray, c: np.ndarray, k: int, metric: int, nthreads: int =
         fn = L.oracle_epilogue_f32 if dt == np.float32 else L.oracle_epilogue_f64
         fn(_p(s), m, n, metric, _p(qn), _p(cn))
     t3 = time.perf_counter()
-    idx, sc = select_topk(s, kk, metric != EUCLIDEAN)
+    idx, sc = select_topk(s, kk, metric != EUCLIDEAN, algo=select)
     t4 = time.perf_counter()
     if timings is not None:
         timings.update(norms=t1 - t0, gemm=t2 - t1, epilogue=t3 - t2, select=t4 - t3)

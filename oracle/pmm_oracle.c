@@ -355,6 +355,199 @@ void oracle_select_topk_f64(const double *s, int64_t m, int64_t n, int64_t k,
     free(e);
 }
 
+/* ---- the reference's per-row select with Rust's own algorithm (timing) ----
+ * src/topk.rs:42-75 per row: a Vec<(usize, f32)> of all N entries (16 bytes
+ * each), `select_nth_unstable_by(k - 1, cmp)`, `truncate(k)`, a stable
+ * `sort_by(cmp)`, with cmp = partial_cmp -> Equal (so is_less(a, b) is
+ * a.score > b.score for higher-is-better, a.score < b.score otherwise; false
+ * whenever a NaN is involved).  select_nth_unstable_by lives in Rust's core
+ * library (core::slice::select, the toolchain's, not vendored; recalled):
+ * introselect over at most 16 rounds of
+ *   - pivot: choose_pivot -- median of 3 at len/8 * {0, 4, 7}, recursively
+ *     (median3_rec) for len >= 64;
+ *   - partition: swap the pivot to the front, a branchless cyclic Lomuto pass
+ *     over the rest (each element moved into the left run, the displaced
+ *     element into the previous position: two moves per element, the
+ *     comparison result added to the run length), pivot swapped to the
+ *     boundary;
+ *   - a chosen pivot not less than the previous round's pivot (runs of equal
+ *     keys): partition by <= and skip the equal run;
+ *   - len <= 16: insertion sort; index 0 / len - 1: a min / max scan;
+ * then a deterministic fallback (median of medians in Rust; a full sort
+ * here -- never reached on the benchmark's random rows).  This is the
+ * CPU baseline's select (oracle.topk_blas, bench.py); the checker keeps
+ * select_k above and its fixed total order.  The two differ only in the
+ * order of equal scores, which the reference leaves unspecified. */
+typedef struct { uint64_t idx; float s; uint32_t pad; } rs_ent;  /* (usize, f32) */
+typedef struct { double s; uint64_t idx; } rs_ent64;            /* (usize, f64) */
+
+#define RS_SELECT_IMPL(NAME, T)                                                              \
+static inline int NAME##_lt(const T *a, const T *b, int desc) {                              \
+    return desc ? (a->s > b->s) : (a->s < b->s);                                             \
+}                                                                                            \
+static inline int NAME##_le(const T *a, const T *b, int desc) { /* !is_less(b, a) */         \
+    return !NAME##_lt(b, a, desc);                                                           \
+}                                                                                            \
+static void NAME##_insertion(T *v, size_t len, int desc) {                                   \
+    for (size_t i = 1; i < len; i++) {                                                       \
+        T x = v[i];                                                                          \
+        size_t j = i;                                                                        \
+        while (j > 0 && NAME##_lt(&x, &v[j - 1], desc)) { v[j] = v[j - 1]; j--; }            \
+        v[j] = x;                                                                            \
+    }                                                                                        \
+}                                                                                            \
+static const T *NAME##_med3(const T *a, const T *b, const T *c, int desc) {                  \
+    int x = NAME##_lt(a, b, desc), y = NAME##_lt(a, c, desc);                                \
+    if (x == y) { int z = NAME##_lt(b, c, desc); return (z ^ x) ? c : b; }                   \
+    return a;                                                                                \
+}                                                                                            \
+static const T *NAME##_med3_rec(const T *a, const T *b, const T *c, size_t n, int desc) {    \
+    if (n * 8 >= 64) {                                                                       \
+        size_t n8 = n / 8;                                                                   \
+        a = NAME##_med3_rec(a, a + n8 * 4, a + n8 * 7, n8, desc);                            \
+        b = NAME##_med3_rec(b, b + n8 * 4, b + n8 * 7, n8, desc);                            \
+        c = NAME##_med3_rec(c, c + n8 * 4, c + n8 * 7, n8, desc);                            \
+    }                                                                                        \
+    return NAME##_med3(a, b, c, desc);                                                       \
+}                                                                                            \
+static size_t NAME##_choose_pivot(const T *v, size_t len, int desc) {                        \
+    size_t n8 = len / 8;                                                                     \
+    const T *p = len < 64 ? NAME##_med3(v, v + n8 * 4, v + n8 * 7, desc)                     \
+                          : NAME##_med3_rec(v, v + n8 * 4, v + n8 * 7, n8, desc);            \
+    return (size_t)(p - v);                                                                  \
+}                                                                                            \
+/* v[0] = pivot; cyclic branchless Lomuto over v[1..len); returns num_lt      \
+ * (one loop per (direction, <= vs <) so the comparison is branch-free) */                   \
+static inline __attribute__((always_inline)) size_t NAME##_part_body(T *w, size_t n, const T *pv, \
+                                                                     const int desc, const int le) { \
+    size_t num_lt = 0;                                                                       \
+    if (n == 0) return 0;                                                                    \
+    const T saved = w[0];                                                                    \
+    T *gap = w;                                                                              \
+    for (size_t i = 1; i < n; i++) {                                                         \
+        T *r = w + i;                                                                        \
+        const int lt = le ? NAME##_le(r, pv, desc) : NAME##_lt(r, pv, desc);                 \
+        T *left = w + num_lt;                                                                \
+        *gap = *left;                                                                        \
+        *left = *r;                                                                          \
+        gap = r;                                                                             \
+        num_lt += (size_t)lt;                                                                \
+    }                                                                                        \
+    const int lt = le ? NAME##_le(&saved, pv, desc) : NAME##_lt(&saved, pv, desc);           \
+    T *left = w + num_lt;                                                                    \
+    *gap = *left;                                                                            \
+    *left = saved;                                                                           \
+    return num_lt + (size_t)lt;                                                              \
+}                                                                                            \
+static size_t NAME##_partition(T *v, size_t len, size_t piv, int desc, int le) {            \
+    T t = v[0]; v[0] = v[piv]; v[piv] = t;                                                   \
+    const T pv = v[0];                                                                       \
+    size_t num_lt;                                                                           \
+    if (desc) num_lt = le ? NAME##_part_body(v + 1, len - 1, &pv, 1, 1)                      \
+                          : NAME##_part_body(v + 1, len - 1, &pv, 1, 0);                     \
+    else num_lt = le ? NAME##_part_body(v + 1, len - 1, &pv, 0, 1)                           \
+                     : NAME##_part_body(v + 1, len - 1, &pv, 0, 0);                          \
+    t = v[0]; v[0] = v[num_lt]; v[num_lt] = t;                                               \
+    return num_lt;                                                                           \
+}                                                                                            \
+static int NAME##_cmp_desc(const void *a, const void *b) {                                   \
+    const T *x = (const T *)a, *y = (const T *)b;                                            \
+    return NAME##_lt(x, y, 1) ? -1 : NAME##_lt(y, x, 1) ? 1 : 0;                             \
+}                                                                                            \
+static int NAME##_cmp_asc(const void *a, const void *b) {                                    \
+    const T *x = (const T *)a, *y = (const T *)b;                                            \
+    return NAME##_lt(x, y, 0) ? -1 : NAME##_lt(y, x, 0) ? 1 : 0;                             \
+}                                                                                            \
+static void NAME##_select_nth(T *v, size_t len, size_t index, int desc) {                    \
+    if (index >= len) return;                                                                \
+    if (index == len - 1 || index == 0) {                                                    \
+        /* max_index / min_index scan: the last (first) position by is_less */               \
+        size_t best = 0;                                                                     \
+        for (size_t i = 1; i < len; i++)                                                     \
+            if (index == 0 ? NAME##_lt(&v[i], &v[best], desc) : !NAME##_lt(&v[i], &v[best], desc)) \
+                best = i;                                                                    \
+        T t = v[index]; v[index] = v[best]; v[best] = t;                                     \
+        return;                                                                              \
+    }                                                                                        \
+    int limit = 16;                                                                          \
+    const T *anc = NULL;                                                                     \
+    T anc_v;                                                                                 \
+    while (1) {                                                                              \
+        if (len <= 16) { if (len >= 2) NAME##_insertion(v, len, desc); return; }             \
+        if (limit == 0) {                                                                    \
+            qsort(v, len, sizeof(T), desc ? NAME##_cmp_desc : NAME##_cmp_asc);               \
+            return;                                                                          \
+        }                                                                                    \
+        limit--;                                                                             \
+        size_t piv = NAME##_choose_pivot(v, len, desc);                                      \
+        if (anc && !NAME##_lt(anc, &v[piv], desc)) {                                         \
+            size_t num_le = NAME##_partition(v, len, piv, desc, 1);                          \
+            if (index <= num_le) return;                                                     \
+            v += num_le + 1; len -= num_le + 1; index -= num_le + 1;                         \
+            anc = NULL;                                                                      \
+            continue;                                                                        \
+        }                                                                                    \
+        size_t num_lt = NAME##_partition(v, len, piv, desc, 0);                              \
+        if (index < num_lt) { len = num_lt; }                                                \
+        else if (index > num_lt) {                                                           \
+            anc_v = v[num_lt]; anc = &anc_v;                                                 \
+            v += num_lt + 1; len -= num_lt + 1; index -= num_lt + 1;                         \
+        } else return;                                                                       \
+    }                                                                                        \
+}                                                                                            \
+/* stable sort of the k kept (Rust's sort_by: insertion sort for short runs) */             \
+static void NAME##_stable_sort(T *v, size_t len, T *tmp, int desc) {                         \
+    if (len <= 20) { NAME##_insertion(v, len, desc); return; }                               \
+    size_t h = len / 2;                                                                      \
+    NAME##_stable_sort(v, h, tmp, desc);                                                     \
+    NAME##_stable_sort(v + h, len - h, tmp, desc);                                           \
+    memcpy(tmp, v, h * sizeof(T));                                                           \
+    size_t i = 0, j = h, o = 0;                                                              \
+    while (i < h && j < len) v[o++] = NAME##_lt(&v[j], &tmp[i], desc) ? v[j++] : tmp[i++];   \
+    while (i < h) v[o++] = tmp[i++];                                                         \
+}
+
+RS_SELECT_IMPL(rs32, rs_ent)
+RS_SELECT_IMPL(rs64, rs_ent64)
+
+void oracle_select_topk_rs_f32(const float *s, int64_t m, int64_t n, int64_t k,
+                               int higher_is_better, uint32_t *out_idx, float *out_score) {
+    if (k <= 0 || n <= 0) return;
+    rs_ent *e = (rs_ent *)malloc(sizeof(rs_ent) * (size_t)n);
+    rs_ent *tmp = (rs_ent *)malloc(sizeof(rs_ent) * (size_t)k);
+    for (int64_t i = 0; i < m; i++) {
+        const float *row = s + i * n;
+        for (int64_t j = 0; j < n; j++) { e[j].idx = (uint64_t)j; e[j].s = row[j]; }  /* enumerate().collect() */
+        rs32_select_nth(e, (size_t)n, (size_t)(k - 1), higher_is_better);
+        rs32_stable_sort(e, (size_t)k, tmp, higher_is_better);
+        for (int64_t j = 0; j < k; j++) {
+            out_idx[i * k + j] = (uint32_t)e[j].idx;
+            out_score[i * k + j] = e[j].s;
+        }
+    }
+    free(tmp);
+    free(e);
+}
+
+void oracle_select_topk_rs_f64(const double *s, int64_t m, int64_t n, int64_t k,
+                               int higher_is_better, uint32_t *out_idx, double *out_score) {
+    if (k <= 0 || n <= 0) return;
+    rs_ent64 *e = (rs_ent64 *)malloc(sizeof(rs_ent64) * (size_t)n);
+    rs_ent64 *tmp = (rs_ent64 *)malloc(sizeof(rs_ent64) * (size_t)k);
+    for (int64_t i = 0; i < m; i++) {
+        const double *row = s + i * n;
+        for (int64_t j = 0; j < n; j++) { e[j].idx = (uint64_t)j; e[j].s = row[j]; }
+        rs64_select_nth(e, (size_t)n, (size_t)(k - 1), higher_is_better);
+        rs64_stable_sort(e, (size_t)k, tmp, higher_is_better);
+        for (int64_t j = 0; j < k; j++) {
+            out_idx[i * k + j] = (uint32_t)e[j].idx;
+            out_score[i * k + j] = e[j].s;
+        }
+    }
+    free(tmp);
+    free(e);
+}
+
 /* metrics.rs:314-365 compute_similarity_matrix_f32 into caller buffer s (m*n) */
 void oracle_similarity_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t d,
                            int metric, float *s, int nthreads) {

@@ -117,6 +117,11 @@ constexpr int drain_tiles() { return KS == 1 ? (PMM_WS_DRAIN_TILES < 2 ? PMM_WS_
 #ifndef PMM_WS_NST
 #define PMM_WS_NST 7  // (A/B override: -DPMM_WS_NST=n)
 #endif
+#ifndef PMM_WS_QPS
+// 1: survivors queued by a per-group wave prefix sum of the lanes' counts
+// (see the epilogue); 0: one ballot round per survivor per lane (round 4)
+#define PMM_WS_QPS 1
+#endif
 #ifndef PMM_WS_MFMA16
 // 1: the MFMA waves (and the seed) on v_mfma_f32_16x16x32_bf16 (default);
 // 0: on v_mfma_f32_32x32x16_bf16 with the K permuted inside each 128-wide
@@ -634,6 +639,44 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
 #pragma unroll
         for (int e = 0; e < 16; e++) bits = (bits << 1) | (uint32_t)!(d[e] < 0.0f);
         if (!any) bits = 0u;
+#if PMM_WS_QPS
+        // every lane's survivor count, one wave prefix sum (5 ballots: a lane
+        // has <= 16), then each lane appends its own survivors at consecutive
+        // queue slots straight from the hand-off registers: no per-survivor
+        // ballot / branch / LDS re-read round.  One capacity check per group,
+        // before the appends.  (The queue order changes, the results do not:
+        // the drain's exact re-score and threshold compare see the same set.)
+        const int nl = __popc(bits);
+        int excl = 0, tot = 0;
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+          const u64 m = __ballot((nl >> j) & 1);
+          excl += lanes_below(m) << j;
+          tot += __popcll(m) << j;
+        }
+        if (qlen + tot > QCAP) {
+          wait_lgkm0();
+          drain();
+        }
+        if (tot <= QCAP) {
+          uint32_t qa = lq_lds + (uint32_t)(qlen + excl) * 8u;
+          const uint32_t hi0 = (uint32_t)(4 * h) | ((uint32_t)gcol << 5);
+#pragma unroll
+          for (int e = 0; e < 16; e++) {
+            if ((bits >> (15 - e)) & 1u) {
+              const uint32_t hi = hi0 + (uint32_t)((e & 3) + 8 * (e >> 2));  // acc_row(e, h) | gcol << 5
+              const u64 item = (u64)__float_as_uint(v4[e >> 2][e & 3]) | ((u64)hi << 32);
+              asm volatile("ds_write_b64 %0, %1" ::"v"(qa), "v"(item) : "memory");
+              qa += 8u;
+            }
+          }
+          qlen += tot;
+          if (timing) cy5 += stamp() - tq0;
+          return;
+        }
+        // (more survivors in this group than the queue holds: a row's first
+        // tiles against an unseeded threshold; the per-round loop below)
+#endif
         const float *hf = (const float *)(hb + ((c * 4) * 64 + lane) * 16);
         for (;;) {
           const bool act = bits != 0u;

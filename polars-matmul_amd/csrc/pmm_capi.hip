@@ -339,7 +339,15 @@ int ff_guess_j() {
   return e ? std::max(1, atoi(e)) : 5;
 }
 int64_t ff_guess_ns(int64_t n) { return std::min<int64_t>(2048, (n / 16) / 32 * 32); }
+// The kernel is not part of the product library (it measured slower than the
+// wave-specialised kernel): it is compiled into
+// libpmm_ff.so (`make ff`, -DPMM_WITH_FF), which the GPU tests load beside
+// libpmm.so as the shipped kernel's bit-exact cross-check.
 bool bf16_ff_enabled(int64_t k, int64_t n, int64_t d) {
+#ifndef PMM_WITH_FF
+  (void)k, (void)n, (void)d;
+  return false;
+#else
   const char *e = getenv("PMM_BF16_FF");
   const int mode = e ? atoi(e) : 0;  // 2 (tests): whenever the kernel can run, however bad the guess
   if (mode == 0) return false;
@@ -348,6 +356,7 @@ bool bf16_ff_enabled(int64_t k, int64_t n, int64_t d) {
   const bool guess_ok = (double)n * ff_guess_j() / (double)ns >= 4.0 * (double)k;
   return ns >= 256 && ns >= ff_guess_j() && (guess_ok || mode == 2) && k + 64 <= 8192 && n < (1 << 26) &&
          gemm_bf16_ff_lds_bytes(dp) > 0 && gemm_bf16_ff_lds_bytes(dp) <= 160 * 1024;
+#endif
 }
 
 int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, Plan &p,
@@ -885,6 +894,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
       }
     }
     if (p.variant == -6) {
+#ifdef PMM_WITH_FF
       // fire-and-forget 256-row kernel: the guessed threshold (the j-th best
       // of an exact ns-row sample, minus 1), the pass, the exact re-score and
       // bucketing into the candidate lists; rows it cannot prove exact are
@@ -908,6 +918,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
         Timed t("ff_bucket", s);
         HIP_TRY(launch_ff_bucket(a, (unsigned *)(w + p.off_fb), (int *)(w + p.off_fb + 16), s));
       }
+#endif
     } else {
       // (the suffix names the kernel; pmm_timing_read matches substrings)
       Timed t(p.variant == -2 ? "gemm_bf16_topk/ws" : "gemm_bf16_topk/one-wave", s);
@@ -951,20 +962,25 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
     Timed t("merge_topk", s);
     HIP_TRY(launch_merge(ma, 0, s));
   }
+#ifdef PMM_WITH_FF
   if (p.variant == -6) {
     int rc = ff_rerun(q, ldq, m, c, ldc, n, d, k, metric, index_base, out_idx, out_score,
                       (const unsigned *)(w + p.off_fb), s, dev);
     if (rc) return rc;
   }
+#endif
   return own ? arena_record(dev, s) : PMM_OK;
 }
 
+#ifdef PMM_WITH_FF
 // The fire-and-forget kernel's rows that it could not prove exact (fewer than
 // k candidates at or above the guessed threshold, or a dropped survivor):
 // their query rows are gathered and re-run on the wave-specialised kernel
 // against the whole corpus, and their lists replace the merge's.  Reads the
-// row count back (a stream synchronisation); rare: the guess leaves about
-// n j / ns scores per row against the k needed.
+// row count back (a stream synchronisation) and allocates the re-run's
+// buffers itself (hipMalloc, outside the caller's workspace): test-library
+// behaviour only (libpmm_ff.so), never in libpmm.so.  Rare: the guess leaves
+// about n j / ns scores per row against the k needed.
 int ff_rerun(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c, int64_t ldc, int64_t n, int64_t d,
              int64_t k, int metric, uint32_t index_base, uint32_t *out_idx, float *out_score, const unsigned *fb,
              hipStream_t s, int dev) {
@@ -1002,6 +1018,7 @@ int ff_rerun(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c, int64
   if (e != hipSuccess) return fail(PMM_ERR_HIP, "ff re-run: %s", hipGetErrorString(e));
   return rc;
 }
+#endif  // PMM_WITH_FF
 
 // Upload a host matrix rows x d into a device buffer with row stride dp,
 // zero-padding columns d..dp-1.
@@ -1409,14 +1426,6 @@ void plan_f64(int64_t m, int64_t n, int64_t k, F64Plan &p) {
   p.total = off;
 }
 
-size_t f64_workspace_bytes(int64_t m, int64_t n, int64_t k, int metric) {
-  (void)metric;
-  F64Plan p;
-  plan_f64(m, n, k, p);
-  MatPlan mp;
-  plan_materialise(m, n, k, 8, mp);
-  return std::max(p.total, mp.total);
-}
 
 // Fused scan or materialised scores, by the size of the M x N f64 score
 // matrix the materialised path writes and re-reads (device API, cosine,
@@ -1432,9 +1441,28 @@ bool f64_fused_enabled(int64_t m, int64_t n) {
   return (double)m * (double)n * 8.0 > kF64FusedMinMatrixBytes;
 }
 
+// Which path a call takes, decided once per call (the workspace is sized for
+// it and the device code follows it, whatever PMM_F64_FUSED says meanwhile).
+bool f64_use_fused(int64_t m, int64_t n, int64_t k) { return k <= kFusedMaxK && f64_fused_enabled(m, n); }
+
+// Workspace of one f64 top-k call: the materialised path's alone when the call
+// takes it; the fused scan's and the materialised path's (its overflow
+// fallback reuses the workspace) otherwise.  (Sizing every call for both held
+// up to 1 GiB of candidate buffers next to a small score matrix.)
+size_t f64_workspace_bytes(int64_t m, int64_t n, int64_t k, bool fused) {
+  MatPlan mp;
+  plan_materialise(m, n, k, 8, mp);
+  if (!fused) return mp.total;
+  F64Plan p;
+  plan_f64(m, n, k, p);
+  return std::max(p.total, mp.total);
+}
+
+// cn_pre: the corpus rows' norms of this metric already on the device (a
+// corpus handle's, computed at creation by the same kernel), else nullptr.
 int topk_f64_materialised(const double *dq, int64_t ldq, int64_t m, const double *dc, int64_t ldc, int64_t n,
                           int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *oi, double *os,
-                          char *w, hipStream_t s) {
+                          char *w, hipStream_t s, const double *cn_pre = nullptr) {
   MatPlan p;
   plan_materialise(m, n, k, 8, p);
   double *qn = (double *)(w + p.off_qn), *cn = (double *)(w + p.off_cn);
@@ -1442,7 +1470,8 @@ int topk_f64_materialised(const double *dq, int64_t ldq, int64_t m, const double
   if (metric != kMetricDot) {
     const int sq = metric == kMetricEuclidean;
     HIP_TRY(launch_norms_f64(dq, m, d, ldq, sq, qn, s));
-    HIP_TRY(launch_norms_f64(dc, n, d, ldc, sq, cn, s));
+    if (cn_pre) cn = (double *)cn_pre;
+    else HIP_TRY(launch_norms_f64(dc, n, d, ldc, sq, cn, s));
   }
   const int64_t dp = cdiv(d, 16) * 16;
   for (int64_t r0 = 0; r0 < m; r0 += p.rows) {
@@ -1477,9 +1506,9 @@ int topk_f64_materialised(const double *dq, int64_t ldq, int64_t m, const double
 
 int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double *dc, int64_t ldc, int64_t n,
                          int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *oi, double *os, char *w,
-                         hipStream_t s) {
-  if (k > kFusedMaxK || !f64_fused_enabled(m, n))
-    return topk_f64_materialised(dq, ldq, m, dc, ldc, n, d, k, metric, index_base, oi, os, w, s);
+                         hipStream_t s, bool fused, const double *cn_pre = nullptr) {
+  if (!fused)
+    return topk_f64_materialised(dq, ldq, m, dc, ldc, n, d, k, metric, index_base, oi, os, w, s, cn_pre);
   F64Plan p;
   plan_f64(m, n, k, p);
   const int64_t dp = cdiv(d, 16) * 16;
@@ -1489,7 +1518,8 @@ int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double 
     const int sq = metric == kMetricEuclidean;
     Timed t("norms_f64", s);
     HIP_TRY(launch_norms_f64(dq, m, d, ldq, sq, qn, s));
-    HIP_TRY(launch_norms_f64(dc, n, d, ldc, sq, cn, s));
+    if (cn_pre) cn = (double *)cn_pre;
+    else HIP_TRY(launch_norms_f64(dc, n, d, ldc, sq, cn, s));
   }
   // chunk schedule: the first chunk fills half a buffer (accept-all), later
   // chunks are g times the columns seen.  After `seen` columns the threshold
@@ -1566,7 +1596,7 @@ int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double 
   unsigned of = 0;
   HIP_TRY(hipMemcpyAsync(&of, flag, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  if (of) return topk_f64_materialised(dq, ldq, m, dc, ldc, n, d, k, metric, index_base, oi, os, w, s);
+  if (of) return topk_f64_materialised(dq, ldq, m, dc, ldc, n, d, k, metric, index_base, oi, os, w, s, cn_pre);
   return PMM_OK;
 }
 
@@ -1594,14 +1624,21 @@ int64_t shard_lo(int64_t n, int G, int g) { return n * g / G; }
 // norms / pre-filter factors of every metric, computed once at creation.
 // With a device list set (pmm_set_devices) the rows are sharded over the
 // devices at creation, one contiguous shard each.
+// A Float64 corpus (pmm_corpus_create_f64; Polars' default float columns
+// take the reference's f64 branch, src/matmul.rs:449-468) keeps its rows in
+// f64 on one device with the f64 norms of both metrics; f64 work is not
+// sharded.
 struct CorpusShard {
   int device = 0;
-  int64_t lo = 0, n = 0;    // rows [lo, lo + n) of the corpus
-  float *data = nullptr;    // n x dp
-  float *norms = nullptr;   // [cosine: n norms | n 1/norm][euclid: n sq | n sq*(1-2^-18)]
+  int64_t lo = 0, n = 0;       // rows [lo, lo + n) of the corpus
+  float *data = nullptr;       // f32: n x dp
+  float *norms = nullptr;      // f32: [cosine: n norms | n 1/norm][euclid: n sq | n sq*(1-2^-18)]
+  double *data64 = nullptr;    // f64: n x dp
+  double *norms64 = nullptr;   // f64: [cosine: n norms][euclid: n sq]
 };
 struct pmm_corpus {
   int64_t n = 0, d = 0, dp = 0;
+  int dtype = PMM_DTYPE_F32;
   std::vector<CorpusShard> shards;
 };
 
@@ -1929,14 +1966,15 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
   size_t off_q = 0, off_c = al256((size_t)m * dp * 8), off_i = off_c + al256((size_t)n * dp * 8);
   size_t off_s = off_i + al256((size_t)m * k * 4), off_w = off_s + al256((size_t)m * k * 8);
   void *base;
-  if ((rc = arena(dev, s, off_w + f64_workspace_bytes(m, n, k, metric), &base))) return rc;
+  const bool fused = f64_use_fused(m, n, k);
+  if ((rc = arena(dev, s, off_w + f64_workspace_bytes(m, n, k, fused), &base))) return rc;
   char *b = (char *)base;
   const double *dq = (const double *)(b + off_q), *dc = (const double *)(b + off_c);
   if ((rc = upload_padded(b + off_q, q, m, d, dp, 8, s))) return rc;
   if ((rc = upload_padded(b + off_c, c, n, d, dp, 8, s))) return rc;
   uint32_t *oi = (uint32_t *)(b + off_i);
   double *os = (double *)(b + off_s);
-  if ((rc = topk_f64_device_impl(dq, dp, m, dc, dp, n, d, k, metric, 0u, oi, os, b + off_w, s))) return rc;
+  if ((rc = topk_f64_device_impl(dq, dp, m, dc, dp, n, d, k, metric, 0u, oi, os, b + off_w, s, fused))) return rc;
   {
     Timed t("d2h", s);
     HIP_TRY(hipMemcpyAsync(out_idx, oi, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
@@ -1964,8 +2002,9 @@ int pmm_topk_f64_device(const double *q, int64_t ldq, int64_t m, const double *c
   if ((rc = ensure_device(&dev))) return rc;
   hipStream_t s = (hipStream_t)stream;
   void *w;
-  if ((rc = arena(dev, s, f64_workspace_bytes(m, n, k, metric), &w))) return rc;
-  rc = topk_f64_device_impl(q, ldq, m, c, ldc, n, d, k, metric, index_base, out_idx, out_score, (char *)w, s);
+  const bool fused = f64_use_fused(m, n, k);
+  if ((rc = arena(dev, s, f64_workspace_bytes(m, n, k, fused), &w))) return rc;
+  rc = topk_f64_device_impl(q, ldq, m, c, ldc, n, d, k, metric, index_base, out_idx, out_score, (char *)w, s, fused);
   if (rc) return rc;
   return arena_record(dev, s);
 }
@@ -2160,11 +2199,13 @@ int pmm_corpus_destroy(pmm_corpus *h) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   for (auto &x : h->shards) {
-    if (!x.data && !x.norms) continue;
+    if (!x.data && !x.norms && !x.data64 && !x.norms64) continue;
     (void)hipSetDevice(x.device);
     (void)hipDeviceSynchronize();
     if (x.data) (void)hipFree(x.data);
     if (x.norms) (void)hipFree(x.norms);
+    if (x.data64) (void)hipFree(x.data64);
+    if (x.norms64) (void)hipFree(x.norms64);
   }
   (void)hipSetDevice(cur);
   delete h;
@@ -2185,9 +2226,101 @@ int pmm_corpus_shards(const pmm_corpus *h, int *shards) {
   return PMM_OK;
 }
 
+int pmm_corpus_dtype(const pmm_corpus *h, int *dtype) {
+  if (!h || !dtype) return fail(PMM_ERR_ARG, "null argument");
+  *dtype = h->dtype;
+  return PMM_OK;
+}
+
+int pmm_corpus_create_f64(const double *c, int64_t n, int64_t d, pmm_corpus **out) {
+  if (!out) return fail(PMM_ERR_ARG, "null argument");
+  *out = nullptr;
+  int rc = validate_sizes(0, n, d, 0, false);
+  if (rc) return rc;
+  if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
+  if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  if (!c) return fail(PMM_ERR_ARG, "null argument");
+  int dev;
+  DevScope scope;
+  if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;  // f64 is not sharded: the list's root
+  hipStream_t s;
+  if ((rc = thread_stream(dev, &s))) return rc;
+  pmm_corpus *h = new pmm_corpus();
+  h->n = n;
+  h->d = d;
+  h->dp = cdiv(d, 16) * 16;  // the f64 kernels' K step (pmm_topk_f64_device's stride rule)
+  h->dtype = PMM_DTYPE_F64;
+  h->shards.resize(1);
+  CorpusShard &x = h->shards[0];
+  x.device = dev;
+  x.lo = 0;
+  x.n = n;
+  hipError_t e = hipMalloc(&x.data64, (size_t)n * h->dp * 8);
+  if (e == hipSuccess) e = hipMalloc(&x.norms64, (size_t)n * 2 * 8);
+  if (e != hipSuccess) {
+    pmm_corpus_destroy(h);
+    return fail(PMM_ERR_HIP, "corpus allocation failed on device %d: %s", dev, hipGetErrorString(e));
+  }
+  if ((rc = upload_padded(x.data64, c, n, d, h->dp, 8, s))) {
+    pmm_corpus_destroy(h);
+    return rc;
+  }
+  // the norms every f64 call would compute (src/metrics.rs:368-379), by the
+  // same kernel on the same padded rows: bit-identical to the per-call ones
+  hipError_t e1 = launch_norms_f64(x.data64, n, d, h->dp, 0, x.norms64, s);
+  hipError_t e2 = launch_norms_f64(x.data64, n, d, h->dp, 1, x.norms64 + n, s);
+  hipError_t e3 = hipStreamSynchronize(s);
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+    pmm_corpus_destroy(h);
+    return fail(PMM_ERR_HIP, "corpus norms failed");
+  }
+  *out = h;
+  return PMM_OK;
+}
+
+int pmm_topk_f64_corpus(const pmm_corpus *h, const double *q, int64_t m, int64_t k, int metric,
+                        uint32_t *out_idx, double *out_score) {
+  if (!h) return fail(PMM_ERR_ARG, "null corpus");
+  if (h->dtype != PMM_DTYPE_F64)
+    return fail(PMM_ERR_ARG, "the corpus handle holds f32 rows: use pmm_topk_f32_corpus");
+  int rc = validate_sizes(m, h->n, h->d, k, true);
+  if (rc) return rc;
+  if ((rc = check_metric(metric))) return rc;
+  if (m == 0 || k == 0) return PMM_OK;
+  const CorpusShard &x = h->shards[0];
+  int dev;
+  DevScope scope;
+  if ((rc = ensure_device(&dev, &scope, x.device))) return rc;
+  hipStream_t s;
+  if ((rc = thread_stream(dev, &s))) return rc;
+  const int64_t dp = h->dp, n = h->n;
+  const bool fused = f64_use_fused(m, n, k);
+  size_t off_q = 0, off_i = al256((size_t)m * dp * 8);
+  size_t off_s = off_i + al256((size_t)m * k * 4), off_w = off_s + al256((size_t)m * k * 8);
+  void *base;
+  if ((rc = arena(dev, s, off_w + f64_workspace_bytes(m, n, k, fused), &base))) return rc;
+  char *b = (char *)base;
+  if ((rc = upload_padded(b + off_q, q, m, h->d, dp, 8, s))) return rc;
+  const double *cn = metric == kMetricCosine ? x.norms64 : metric == kMetricEuclidean ? x.norms64 + n : nullptr;
+  uint32_t *oi = (uint32_t *)(b + off_i);
+  double *os = (double *)(b + off_s);
+  rc = topk_f64_device_impl((const double *)(b + off_q), dp, m, x.data64, dp, n, h->d, k, metric, 0u, oi, os,
+                            b + off_w, s, fused, cn);
+  if (rc) return rc;
+  {
+    Timed t("d2h", s);
+    HIP_TRY(hipMemcpyAsync(out_idx, oi, (size_t)m * k * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(out_score, os, (size_t)m * k * 8, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  return PMM_OK;
+}
+
 int pmm_topk_f32_corpus(const pmm_corpus *h, const float *q, int64_t m, int64_t k, int metric,
                         uint32_t *out_idx, float *out_score) {
   if (!h) return fail(PMM_ERR_ARG, "null corpus");
+  if (h->dtype != PMM_DTYPE_F32)
+    return fail(PMM_ERR_ARG, "the corpus handle holds f64 rows: use pmm_topk_f64_corpus");
   int rc = validate_sizes(m, h->n, h->d, k, true);
   if (rc) return rc;
   if ((rc = check_metric(metric))) return rc;

@@ -10,6 +10,7 @@ RuntimeError with the library's message.
 """
 from __future__ import annotations
 
+import atexit
 import collections
 import ctypes
 import importlib.util
@@ -66,10 +67,13 @@ EXPORTED_SYMBOLS = (
     "pmm_norms_f32_device",
     "pmm_norms_f64_device",
     "pmm_corpus_create_f32",
+    "pmm_corpus_create_f64",
+    "pmm_corpus_dtype",
     "pmm_corpus_destroy",
     "pmm_corpus_info",
     "pmm_corpus_shards",
     "pmm_topk_f32_corpus",
+    "pmm_topk_f64_corpus",
     "pmm_timing_enable",
     "pmm_timing_reset",
     "pmm_timing_read",
@@ -149,6 +153,8 @@ _SIGS = {
     "pmm_norms_f32_device": ([_vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_norms_f64_device": ([_vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_corpus_create_f32": ([_vp, _i64, _i64, ctypes.POINTER(ctypes.c_void_p)], _i32),
+    "pmm_corpus_create_f64": ([_vp, _i64, _i64, ctypes.POINTER(ctypes.c_void_p)], _i32),
+    "pmm_corpus_dtype": ([_vp, ctypes.POINTER(ctypes.c_int)], _i32),
     "pmm_corpus_destroy": ([_vp], _i32),
     "pmm_corpus_info": (
         [_vp, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int)],
@@ -156,6 +162,7 @@ _SIGS = {
     ),
     "pmm_corpus_shards": ([_vp, ctypes.POINTER(ctypes.c_int)], _i32),
     "pmm_topk_f32_corpus": ([_vp, _vp, _i64, _i64, _i32, _vp, _vp], _i32),
+    "pmm_topk_f64_corpus": ([_vp, _vp, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_timing_enable": ([_i32], _i32),
     "pmm_timing_reset": ([], _i32),
     "pmm_timing_read": (
@@ -306,6 +313,7 @@ class PinnedPool:
         self.idle = 0
         self.lock = threading.Lock()
         self.returned = collections.deque()  # (ptr, nbytes) from finalisers, lock-free
+        self.pending = 0  # bytes waiting in `returned` (approximate: updated without the lock)
 
     def _absorb(self):
         """Move finalised blocks into the free lists (lock held by caller).
@@ -317,6 +325,7 @@ class PinnedPool:
                 p, nbytes = self.returned.popleft()
             except IndexError:
                 return over
+            self.pending -= nbytes
             if self.idle + nbytes <= self.cap:
                 self.free.setdefault(nbytes, []).append(p)
                 self.idle += nbytes
@@ -345,8 +354,29 @@ class PinnedPool:
         return p, _PinnedBlock(p, nbytes, self)
 
     def _give_back(self, p: int, nbytes: int) -> None:
-        # runs from finalisers: no lock, no allocation beyond the deque node
+        # runs from finalisers: never waits on the lock (the finaliser may run
+        # inside `take` on the thread that holds it), allocates nothing beyond
+        # the deque node before it tries the lock
+        self.pending += nbytes
         self.returned.append((p, nbytes))
+        # opportunistic drain: blocks past the cap are freed as they come back,
+        # not left page-locked until a later take(); when the lock
+        # is busy, its holder or the next call drains them
+        self.drain(blocking=False)
+
+    def drain(self, blocking: bool = True) -> None:
+        """Move returned blocks into the free lists and free those past the cap."""
+        if not self.lock.acquire(blocking=blocking):
+            return
+        try:
+            over = self._absorb()
+        finally:
+            self.lock.release()
+        for q in over:
+            _lib.pmm_host_free(q)
+
+    def pending_bytes(self) -> int:
+        return max(0, self.pending)
 
     def idle_bytes(self) -> int:
         with self.lock:
@@ -367,6 +397,7 @@ class PinnedPool:
 
 
 pinned_pool = PinnedPool(int(os.environ.get("PMM_PINNED_POOL_BYTES", str(1 << 30))))
+atexit.register(pinned_pool.clear)  # idle page-locked blocks go back to the OS at exit
 
 
 def pinned_empty(shape, dtype) -> np.ndarray:
@@ -469,16 +500,27 @@ def timing_read(kernel: str):
     return ms.value, n.value
 
 
-def corpus_device_bytes(n: int, d: int) -> int:
-    """HBM a DeviceCorpus of n x d f32 rows holds (pmm_corpus_create_f32): the
-    rows padded to a multiple of 32 floats plus four norm arrays (cosine norms
-    and pre-filter factors, euclidean squared norms and factors)."""
+DTYPE_F32 = 0
+DTYPE_F64 = 1
+
+
+def corpus_device_bytes(n: int, d: int, dtype=np.float32) -> int:
+    """HBM a DeviceCorpus of n x d rows holds.  f32 (pmm_corpus_create_f32):
+    the rows padded to a multiple of 32 floats plus four norm arrays (cosine
+    norms and pre-filter factors, euclidean squared norms and factors).  f64
+    (pmm_corpus_create_f64): the rows padded to a multiple of 16 doubles plus
+    two norm arrays (cosine norms, euclidean squared norms)."""
+    if np.dtype(dtype) == np.float64:
+        dp = -(-d // 16) * 16
+        return n * dp * 8 + n * 2 * 8
     dp = -(-d // 32) * 32
     return n * dp * 4 + n * 4 * 4
 
 
 class DeviceCorpus:
-    """An f32 corpus uploaded once to HBM with its norms (pmm_corpus_*).
+    """A corpus uploaded once to HBM with its norms (pmm_corpus_*), f32 or f64
+    rows by the dtype of ``c`` (the reference's two branches,
+    src/matmul.rs:427-468).
 
     Reference-counted: ``acquire()`` / ``release()`` bracket a use (``topk``
     does so itself); ``close()`` frees the device memory at once if no use is
@@ -486,15 +528,17 @@ class DeviceCorpus:
     handle while another thread is still searching it."""
 
     def __init__(self, c: np.ndarray):
-        c = np.ascontiguousarray(c, dtype=np.float32)
+        self.dtype = np.dtype(np.float64 if np.asarray(c).dtype == np.float64 else np.float32)
+        c = np.ascontiguousarray(c, dtype=self.dtype)
         h = ctypes.c_void_p()
-        check(_lib.pmm_corpus_create_f32(ptr(c), c.shape[0], c.shape[1], ctypes.byref(h)))
+        create = _lib.pmm_corpus_create_f64 if self.dtype == np.float64 else _lib.pmm_corpus_create_f32
+        check(create(ptr(c), c.shape[0], c.shape[1], ctypes.byref(h)))
         self._h = h
         self._lock = threading.Lock()
         self._refs = 0
         self._closing = False
         self.n, self.d = c.shape
-        self.nbytes = corpus_device_bytes(self.n, self.d)  # device footprint, not host bytes
+        self.nbytes = corpus_device_bytes(self.n, self.d, self.dtype)  # device footprint, not host bytes
 
     def acquire(self) -> "DeviceCorpus":
         with self._lock:
@@ -510,15 +554,18 @@ class DeviceCorpus:
                 self._destroy()
 
     def topk(self, q: np.ndarray, k: int, metric: int):
-        q = np.ascontiguousarray(q, dtype=np.float32)
+        """(idx uint32 (m, k), scores (m, k) in the corpus dtype); q is
+        converted to the corpus dtype."""
+        q = np.ascontiguousarray(q, dtype=self.dtype)
         if q.shape[1] != self.d:
             raise ValueError("dimension mismatch")
         m = q.shape[0]
         idx = np.empty((m, k), dtype=np.uint32)
-        sc = np.empty((m, k), dtype=np.float32)
+        sc = np.empty((m, k), dtype=self.dtype)
+        fn = _lib.pmm_topk_f64_corpus if self.dtype == np.float64 else _lib.pmm_topk_f32_corpus
         self.acquire()
         try:
-            check(_lib.pmm_topk_f32_corpus(self._h, ptr(q), m, k, metric, ptr(idx), ptr(sc)))
+            check(fn(self._h, ptr(q), m, k, metric, ptr(idx), ptr(sc)))
         finally:
             self.release()
         return idx, sc
@@ -534,6 +581,13 @@ class DeviceCorpus:
         n = ctypes.c_int(0)
         check(_lib.pmm_corpus_shards(self._h, ctypes.byref(n)))
         return n.value
+
+    @property
+    def device_dtype(self) -> int:
+        """DTYPE_F32 / DTYPE_F64 as the library reports it (pmm_corpus_dtype)."""
+        v = ctypes.c_int(-1)
+        check(_lib.pmm_corpus_dtype(self._h, ctypes.byref(v)))
+        return v.value
 
     @property
     def closed(self) -> bool:

@@ -191,7 +191,8 @@ def _as_usize(k) -> int:
 
 
 # ---------------------------------------------------------------------------
-# Device-resident corpus cache.  Polars' map_batches may
+# Device-resident corpus cache, for both branches of the
+# reference (f32 and f64 rows; src/matmul.rs:427-468).  Polars' map_batches may
 # call _topk repeatedly with the same corpus Series.  Only corpora that came
 # in as Polars Series or Arrow arrays are cached (their buffers persist across
 # calls; a Python list or numpy matrix is rebuilt or mutable, so it would only
@@ -245,8 +246,11 @@ def _cached_corpus(original, rv, c: np.ndarray):
         return None
     key = _arrow_key(rv)
     if key is not None:
-        key = key + (tuple(_native.get_devices()),)  # a handle is sharded over the list of its creation
-    dev_bytes = _native.corpus_device_bytes(c.shape[0], c.shape[1])
+        # the compute dtype: an f32 column searched by f64 queries runs the
+        # f64 branch (src/matmul.rs:427) on an f64 copy of the same buffers;
+        # a handle is sharded over the device list of its creation
+        key = key + (c.dtype.str, tuple(_native.get_devices()))
+    dev_bytes = _native.corpus_device_bytes(c.shape[0], c.shape[1], c.dtype)
     if not _CACHE_ON or key is None or c.nbytes < _CACHE_MIN_BYTES or dev_bytes > _CACHE_BYTES:
         return None
     with _cache_lock:
@@ -366,10 +370,11 @@ def _topk(left, right, k, metric):
         sc = np.zeros((m, 0), dtype=np.float64)
     else:
         _apply_devices_env()
-        # (a handle sharded over several GPUs serves k <= 1024; larger k runs
-        # on one GPU, the device list's first)
+        # (an f32 handle sharded over several GPUs serves k <= 1024; larger k
+        # runs on one GPU, the device list's first.  An f64 handle lives on
+        # one GPU and serves any k.)
         dc = (_cached_corpus(right, rv, c)
-              if use_f32 and (kk <= 1024 or len(_native.get_devices()) <= 1) else None)
+              if (not use_f32 or kk <= 1024 or len(_native.get_devices()) <= 1) else None)
         if dc is not None:
             try:
                 idx, sc = dc.topk(q, kk, metric_id)

@@ -55,3 +55,54 @@ def test_early_spawner_runs_a_program_and_returns_its_output():
     sp.close()  # already used: no-op
     unused = bench.EarlySpawner()
     unused.close()  # the helper exits without running anything
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(ROOT, "bench.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_summary_is_the_last_key_and_carries_every_extra():
+    # the driver keeps only the tail of stdout; the line's
+    # last key digests the headline and every extra
+    b = _bench_module()
+    line = {
+        "value": 93000.0, "ms_per_step": 1070.0, "config": {"workload": "c3"},
+        "roofline": {"frac": 0.91, "kernel_ms_avg": 1068.0},
+        "cpu_baseline": {"value": 176.0, "unit": "queries/s", "cores": 16},
+        "extra": {
+            "c4": {"value": 700000.0, "ms_per_step": 140.0, "roofline": {"frac": 0.45, "kernel_ms_avg": 134.0}},
+            "c1": {"value": 1e7, "ms_per_step": 0.1, "roofline": {"frac": 0.31},
+                   "boundary": {"f32_list_cached": {"ms_per_call": 0.5, "split_ms": {"h2d": 0.04}},
+                                "reps": 5},
+                   "small_kernels": {"prologue": {"us_avg": 17.0}, "fused_us_avg": 72.0}},
+            "c1_f64": {"default": {"value": 3e6, "ms_per_step": 0.3, "roofline": {"frac": 0.1}},
+                       "fused": {"ms_per_step": 0.35}, "materialised": {"ms_per_step": 0.3}},
+            "matmul": {"value": 900.0, "ms_per_call": 1.1},
+            "c5_rank": {"value": 55000.0, "ms_per_step": 18000.0, "roofline": {"frac": 0.9}},
+        },
+    }
+    line["summary"] = b.summary_of(line)
+    text = json.dumps(line)
+    assert list(json.loads(text))[-1] == "summary"
+    sm = line["summary"]
+    assert set(sm) >= {"headline", "c4", "c1", "c1_f64", "matmul", "c5_rank", "cpu_baseline"}
+    assert sm["c4"]["frac"] == 0.45 and sm["c5_rank"]["ms_per_step"] == 18000.0
+    assert sm["c1"]["e2e_ms"] == {"f32_list_cached": 0.5} and sm["c1"]["small_kernels_us"]["prologue"] == 17.0
+    assert sm["c1_f64"]["fused_ms"] == 0.35 and sm["matmul"]["ms_per_call"] == 1.1
+    assert len(json.dumps(sm)) < 4000
+
+
+def test_descendants_names_a_live_child():
+    b = _bench_module()
+    p = subprocess.Popen([sys.executable, "-c", "import time; time.sleep(30)"])
+    try:
+        kids = b.descendants(os.getpid())
+        assert any(k == p.pid and "sleep" in c for k, _, c in kids), kids
+    finally:
+        p.kill()
+        p.wait()

@@ -323,6 +323,10 @@ def test_corpus_cache_sizes_entries_by_device_footprint():
     # norm arrays, so d = 72 takes 96 floats per row on the device
     assert _native.corpus_device_bytes(1000, 72) == 1000 * 96 * 4 + 1000 * 16
     assert _native.corpus_device_bytes(10, 32) == 10 * 32 * 4 + 10 * 16
+    # an f64 corpus (pmm_corpus_create_f64): rows padded to 16 doubles, two
+    # f64 norm arrays
+    assert _native.corpus_device_bytes(1000, 70, np.float64) == 1000 * 80 * 8 + 1000 * 16
+    assert _native.corpus_device_bytes(10, 16, np.float64) == 10 * 16 * 8 + 10 * 16
 
 
 def test_device_list_parse_and_validation():
@@ -417,3 +421,45 @@ def test_pinned_pool_finaliser_inside_take_does_not_deadlock(monkeypatch):
     t = pool.take(3 << 20)  # allocates; the stub finalises the 2 MiB block inside
     assert t is not None
     assert pool.idle_bytes() == 2 << 20
+
+
+def test_pinned_pool_frees_over_cap_blocks_without_a_later_take(monkeypatch):
+    # blocks returned past the pool's cap are freed when they
+    # come back (an opportunistic, non-blocking drain in the finaliser path),
+    # not only on the next take(): a burst of large results freed at the end of
+    # a workload does not stay page-locked
+    import gc
+
+    store = {}
+    frees = []
+
+    class StubLib:
+        def pmm_host_alloc(self, nbytes, out):
+            b = ctypes.create_string_buffer(nbytes)
+            store[ctypes.addressof(b)] = b
+            out._obj.value = ctypes.addressof(b)
+            return 0
+
+        def pmm_host_free(self, p):
+            frees.append(p)
+            return 0
+
+    monkeypatch.setattr(_native, "_lib", StubLib())
+    pool = _native.PinnedPool(3 << 20)  # holds at most one 2 MiB block idle
+    monkeypatch.setattr(_native, "pinned_pool", pool)
+    arrs = [_native.pinned_empty((512, 1024), np.float32) for _ in range(4)]  # 2 MiB each
+    ptrs = [a.ctypes.data for a in arrs]
+    del arrs
+    gc.collect()
+    # no take() since: one block kept idle, the other three already freed
+    assert len(frees) == 3 and set(frees) < set(ptrs)
+    assert pool.pending_bytes() == 0 and pool.idle == 2 << 20
+    # a block returned while the pool's lock is held (a finaliser inside
+    # take) waits in the deque, counted, and is handled by the next drain
+    with pool.lock:
+        pool._give_back(999, 2 << 20)
+        assert pool.pending_bytes() == 2 << 20
+    pool.drain()
+    assert 999 in frees and pool.pending_bytes() == 0
+    pool.clear()
+    assert len(frees) == 4 + 1

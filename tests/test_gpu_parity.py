@@ -702,6 +702,107 @@ def test_arrow_corpus_cache_through_extension(pmm):
     assert len(ext._cache) == 0
 
 
+# ---- Float64 corpus handles (SURVEY 8f rank 4 for the
+# reference's f64 branch, src/matmul.rs:449-468): the rows and their f64 norms
+# stay in HBM; each call uploads only the queries ----
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_f64_device_corpus_handle_matches_host_api(pmm, fused, monkeypatch):
+    n = _native()
+    monkeypatch.setenv("PMM_F64_FUSED", fused)
+    rs = np.random.RandomState(31)
+    q = rs.randn(120, 70)
+    c = rs.randn(5000, 70)
+    c[4000:4030] = c[:30]  # exact ties
+    c[77] = 0.0            # a zero-norm row (cosine score 0, src/metrics.rs:277-288)
+    dc = n.DeviceCorpus(c)
+    assert dc.dtype == np.float64 and dc.device_dtype == n.DTYPE_F64
+    for metric in ("cosine", "dot", "euclidean"):
+        for k in (1, 25, 1100):  # 1100 > 1024: the materialised path either way
+            want_i, want_s = n.topk_host(q, c, k, METRICS[metric])
+            got_i, got_s = dc.topk(q, k, METRICS[metric])
+            assert got_s.dtype == np.float64
+            assert np.array_equal(got_i, want_i), (metric, k)
+            assert np.array_equal(got_s.view(np.uint64), want_s.view(np.uint64)), (metric, k)
+        oi, osc = oracle.topk(q[:24], c, 25, METRICS[metric])
+        gi, gs = dc.topk(q[:24], 25, METRICS[metric])
+        assert np.array_equal(gi, oi), metric
+        np.testing.assert_allclose(gs, osc, rtol=1e-12, atol=1e-12)
+    dc.close()
+
+
+def test_f64_corpus_handle_fused_scan_uses_cached_norms(pmm, monkeypatch):
+    # a shape the library scans fused by size (m x n x 8 B > 256 MB): no corpus
+    # norm launch per call -- only the queries' -- and the same lists as the
+    # host API, which computes both
+    n = _native()
+    rs = np.random.RandomState(32)
+    q, c = rs.randn(300, 48), rs.randn(120_000, 48)
+    dc = n.DeviceCorpus(c)
+    want = n.topk_host(q, c, 10, METRICS["cosine"])
+    n.timing_reset()
+    n.timing_enable(True)
+    try:
+        got = dc.topk(q, 10, METRICS["cosine"])
+    finally:
+        n.timing_enable(False)
+    assert n.timing_read("gemm_f64_topk")[1] >= 1 and n.timing_read("gemm_f64_scores")[1] == 0
+    h2d_ms, h2d_n = n.timing_read("h2d")
+    assert h2d_n == 1  # the queries only
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1].view(np.uint64), want[1].view(np.uint64))
+    dc.close()
+
+
+def test_corpus_handle_dtype_mismatch_raises(pmm):
+    n = _native()
+    rs = np.random.RandomState(33)
+    c32 = rs.randn(300, 16).astype(np.float32)
+    c64 = c32.astype(np.float64)
+    h32, h64 = n.DeviceCorpus(c32), n.DeviceCorpus(c64)
+    assert h32.device_dtype == n.DTYPE_F32 and h64.device_dtype == n.DTYPE_F64
+    q64 = np.ascontiguousarray(rs.randn(4, 16))
+    q32 = q64.astype(np.float32)
+    idx = np.empty((4, 5), np.uint32)
+    for fn, h, q, sc in ((n.lib().pmm_topk_f64_corpus, h32, q64, np.empty((4, 5))),
+                         (n.lib().pmm_topk_f32_corpus, h64, q32, np.empty((4, 5), np.float32))):
+        rc = fn(h._h, n.ptr(q), 4, 5, 0, n.ptr(idx), n.ptr(sc))
+        assert rc == n.PMM_ERR_ARG and "corpus handle holds" in n.last_error()
+    h32.close()
+    h64.close()
+
+
+def test_arrow_f64_corpus_cache_through_extension(pmm):
+    # Polars' default Float64 column as the corpus: cached on the device like
+    # an f32 one (one entry, hit on the second batch), the results the host
+    # API's; the same buffers searched by f32 queries (-> the f64 branch,
+    # src/matmul.rs:427) and by f64 ones share the f64 entry, while an f32
+    # column searched by f32 queries is its own (f32) entry
+    from polars_matmul import _polars_matmul as ext
+
+    ext.clear_corpus_cache()
+    rs = np.random.RandomState(34)
+    c = rs.randn(5000, 64)  # 2.6 MB of f64 (1.3 MB as f32): cached either way
+    carr = pa.FixedSizeListArray.from_arrays(pa.array(c.reshape(-1)), 64)
+    q1 = pa.FixedSizeListArray.from_arrays(pa.array(rs.randn(40 * 64)), 64)
+    q2 = pa.FixedSizeListArray.from_arrays(pa.array(rs.randn(30 * 64).astype(np.float32)), 64)
+    r1 = ext._topk(q1, carr, 12, "cosine")
+    assert len(ext._cache) == 1
+    r2 = ext._topk(q2, carr, 12, "euclidean")
+    assert len(ext._cache) == 1  # same corpus, same compute dtype: a hit
+    (key, (_, dc)), = ext._cache.items()
+    assert dc.dtype == np.float64
+    for qa, r, metric in ((q1, r1, "cosine"), (q2, r2, "euclidean")):
+        qn = np.asarray(qa.values).reshape(-1, 64).astype(np.float64)
+        want_i, want_s = gpu_topk(qn, c, 12, metric)
+        got = r.to_pylist()
+        assert [[x["index"] for x in row] for row in got] == want_i.tolist()
+        assert [[x["score"] for x in row] for row in got] == want_s.tolist()
+    c32 = pa.FixedSizeListArray.from_arrays(pa.array(c.reshape(-1).astype(np.float32)), 64)
+    ext._topk(q2, c32, 12, "cosine")
+    assert len(ext._cache) == 2 and sorted(v[1].dtype.str for v in ext._cache.values()) == ["<f4", "<f8"]
+    ext.clear_corpus_cache()
+    assert len(ext._cache) == 0
+
+
 # ---------------------------------------------------------------------------
 # bf16 compute path (PMM_COMPUTE_BF16, BASELINE configs[3]).  Truth = the
 # metric of the bf16-rounded rows in float64; the device accumulates the
@@ -709,8 +810,8 @@ def test_arrow_corpus_cache_through_extension(pmm):
 # |q||c|-scaled dot term).  SURVEY 8c's own bar for bf16 (recall@k >= 0.95
 # vs the f32 result) is checked separately.
 # ---------------------------------------------------------------------------
-def gpu_topk_bf16(q, c, k, metric):
-    n = _native()
+def gpu_topk_bf16(q, c, k, metric, n=None):
+    n = n or _native()
     kk = min(k, c.shape[0])
     return n.topk_host(np.ascontiguousarray(q, dtype=np.float32),
                        np.ascontiguousarray(c, dtype=np.float32), kk, METRICS[metric],
@@ -1180,24 +1281,68 @@ def test_set_devices_distinct_gpus(pmm, device_list, metric):
 # replaced the lab-only r64 kernel's, which ran the 32x32x16 chain).  Every
 # list also passes the bf16 truth check (the exact top-k of the rounded rows
 # up to f32 summation order). ----
-def _ws_and_ff(q, c, k, metric, monkeypatch, ff="1"):
+# The ff kernel is not in the product library: it lives in the test library
+# libpmm_ff.so (`make ff`; the product's sources plus the ff kernel), bound
+# here as a second ctypes module beside libpmm.so.  The shipped results come
+# from libpmm.so, the cross-check's from libpmm_ff.so with PMM_BF16_FF set.
+@pytest.fixture(scope="module")
+def ffn(pmm):
+    import importlib.util
+
+    from polars_matmul import _native as base
+
+    path = os.path.join(os.path.dirname(base.__file__), "libpmm_ff.so")
+    assert os.path.exists(path), "libpmm_ff.so not built (make -C polars-matmul_amd ff)"
+    spec = importlib.util.spec_from_file_location("polars_matmul._native_ff", base.__file__)
+    mod = importlib.util.module_from_spec(spec)
+    old = os.environ.get("PMM_LIB")
+    os.environ["PMM_LIB"] = "libpmm_ff.so"
+    try:
+        spec.loader.exec_module(mod)
+    finally:
+        if old is None:
+            os.environ.pop("PMM_LIB", None)
+        else:
+            os.environ["PMM_LIB"] = old
+    assert mod.LIB_PATH.endswith("libpmm_ff.so") and mod.lib() is not base.lib()
+    return mod
+
+
+def _ws_and_ff(q, c, k, metric, monkeypatch, ffn, ff="1"):
     monkeypatch.setenv("PMM_BF16_FF", ff)
-    fi, fsc = gpu_topk_bf16(q, c, k, metric)
+    fi, fsc = gpu_topk_bf16(q, c, k, metric, n=ffn)
     monkeypatch.setenv("PMM_BF16_FF", "0")
     wi, wsc = gpu_topk_bf16(q, c, k, metric)
     return (fi, fsc), (wi, wsc)
 
 
+def test_product_library_has_no_ff_kernel(pmm, ffn, monkeypatch):
+    # PMM_BF16_FF has no effect on libpmm.so (the kernel is not compiled in):
+    # no "gemm_bf16_topk/ff" launch there, one in the test library
+    rs = np.random.RandomState(3)
+    q = rs.randn(300, 256).astype(np.float32)
+    c = rs.randn(70000, 256).astype(np.float32)
+    monkeypatch.setenv("PMM_BF16_FF", "1")
+    for lib, want in ((_native(), 0), (ffn, 1)):
+        lib.timing_reset()
+        lib.timing_enable(True)
+        try:
+            gpu_topk_bf16(q, c, 10, "cosine", n=lib)
+        finally:
+            lib.timing_enable(False)
+        assert lib.timing_read("gemm_bf16_topk/ff")[1] == want
+
+
 @pytest.mark.parametrize("m,n,d,k", [(300, 70000, 256, 10), (520, 200000, 768, 100), (257, 131072, 384, 32),
                                      (1000, 100003, 128, 20), (70, 90000, 640, 8), (33, 66000, 500, 16)])
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-def test_bf16_ff_equals_ws(pmm, m, n, d, k, metric, monkeypatch):
+def test_bf16_ff_equals_ws(pmm, ffn, m, n, d, k, metric, monkeypatch):
     rs = np.random.RandomState(m + n + d + k + 13)
     q = rs.randn(m, d).astype(np.float32)
     c = rs.randn(n, d).astype(np.float32)
     c[n // 2:n // 2 + 20] = c[:20]  # exact ties across the corpus
     q[m // 2] = 0.0                  # a zero-norm query row
-    (fi, fsc), (wi, wsc) = _ws_and_ff(q, c, k, metric, monkeypatch)
+    (fi, fsc), (wi, wsc) = _ws_and_ff(q, c, k, metric, monkeypatch, ffn)
     _bf16_truth_check(q, c, k, metric, fi, fsc, f"bf16 ff {m}x{n}x{d} k={k} {metric}")
     assert np.array_equal(fi, wi)
     assert np.array_equal(fsc.view(np.uint32), wsc.view(np.uint32))
@@ -1206,7 +1351,7 @@ def test_bf16_ff_equals_ws(pmm, m, n, d, k, metric, monkeypatch):
 @pytest.mark.parametrize("m,n,d,k", [(300, 5000, 256, 10), (70, 3000, 500, 192), (257, 20011, 768, 100),
                                      (1, 1000, 256, 1), (600, 999, 700, 64), (130, 9000, 384, 120)])
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-def test_bf16_ff_forced_equals_ws_small(pmm, m, n, d, k, metric, monkeypatch):
+def test_bf16_ff_forced_equals_ws_small(pmm, ffn, m, n, d, k, metric, monkeypatch):
     # corpora too short for the ff kernel's guess (PMM_BF16_FF=2 runs it
     # anyway): most rows are re-run on the shipped kernel, the rest must
     # match it bit for bit; odd D (zero-padded to 128), k up to 192, one row
@@ -1215,13 +1360,13 @@ def test_bf16_ff_forced_equals_ws_small(pmm, m, n, d, k, metric, monkeypatch):
     c = rs.randn(n, d).astype(np.float32)
     c[n // 2:n // 2 + 20] = c[:20]
     q[m // 2] = 0.0
-    (fi, fsc), (wi, wsc) = _ws_and_ff(q, c, min(k, n), metric, monkeypatch, ff="2")
+    (fi, fsc), (wi, wsc) = _ws_and_ff(q, c, min(k, n), metric, monkeypatch, ffn, ff="2")
     assert np.array_equal(fi, wi)
     assert np.array_equal(fsc.view(np.uint32), wsc.view(np.uint32))
 
 
 @pytest.mark.parametrize("metric", ["cosine", "euclidean", "dot"])
-def test_bf16_ws_whole_blocks_equal_ff(pmm, metric, monkeypatch):
+def test_bf16_ws_whole_blocks_equal_ff(pmm, ffn, metric, monkeypatch):
     # PMM_CUS=16: 258 query blocks of 128 rows on 16 workgroups, so 256 run
     # whole on the shipped kernel (row state carried across splits) and two
     # as split units; the ff kernel runs split units only: bit-equal
@@ -1238,9 +1383,10 @@ def test_bf16_ws_whole_blocks_equal_ff(pmm, metric, monkeypatch):
     outs = []
     for ff in ("2", "0"):
         monkeypatch.setenv("PMM_BF16_FF", ff)
+        lib = ffn if ff != "0" else n
         oi = torch.empty((m, k), dtype=torch.int32, device=dev)
         osc = torch.empty((m, k), dtype=torch.float32, device=dev)
-        n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS[metric],
+        lib.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS[metric],
                            oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         outs.append((oi.cpu().numpy(), osc.cpu().numpy()))
@@ -1248,7 +1394,7 @@ def test_bf16_ws_whole_blocks_equal_ff(pmm, metric, monkeypatch):
     assert np.array_equal(outs[0][1].view(np.uint32), outs[1][1].view(np.uint32))
 
 
-def test_bf16_ws_seeded_300k_rows_equal_ff(pmm, monkeypatch):
+def test_bf16_ws_seeded_300k_rows_equal_ff(pmm, ffn, monkeypatch):
     # a corpus long enough for the threshold seed (n >= 8 ns) and for
     # compactions, queue overflows and catch-ups in early tiles: bit-equal
     import torch
@@ -1263,9 +1409,10 @@ def test_bf16_ws_seeded_300k_rows_equal_ff(pmm, monkeypatch):
     outs = []
     for ff in ("1", "0"):
         monkeypatch.setenv("PMM_BF16_FF", ff)
+        lib = ffn if ff != "0" else n
         oi = torch.empty((m, k), dtype=torch.int32, device=dev)
         osc = torch.empty((m, k), dtype=torch.float32, device=dev)
-        n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS["cosine"],
+        lib.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS["cosine"],
                            oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         outs.append((oi.cpu().numpy(), osc.cpu().numpy()))
@@ -1275,7 +1422,7 @@ def test_bf16_ws_seeded_300k_rows_equal_ff(pmm, monkeypatch):
 
 @pytest.mark.parametrize("knobs", [{"PMM_FF_J": "1"}, {"PMM_FF_CAP": "256"}, {"PMM_FF_J": "1", "PMM_FF_CAP": "64"}])
 @pytest.mark.parametrize("metric", ["cosine", "euclidean"])
-def test_bf16_ff_reruns_rows_it_cannot_prove(pmm, knobs, metric, monkeypatch):
+def test_bf16_ff_reruns_rows_it_cannot_prove(pmm, ffn, knobs, metric, monkeypatch):
     # a guess at the sample's best (j = 1: about n / ns scores per row pass,
     # fewer than k for many rows) and/or survivor regions far too small
     # (dropped items): the affected rows must be re-run, and every list must
@@ -1287,7 +1434,7 @@ def test_bf16_ff_reruns_rows_it_cannot_prove(pmm, knobs, metric, monkeypatch):
     monkeypatch.setenv("PMM_BF16_FF", "2")  # forced, whatever the guess leaves
     for kk, v in knobs.items():
         monkeypatch.setenv(kk, v)
-    fi, fsc = gpu_topk_bf16(q, c, k, metric)
+    fi, fsc = gpu_topk_bf16(q, c, k, metric, n=ffn)
     _bf16_truth_check(q, c, k, metric, fi, fsc, f"bf16 ff rerun {knobs} {metric}")
     for kk in knobs:
         monkeypatch.delenv(kk)
@@ -1297,13 +1444,13 @@ def test_bf16_ff_reruns_rows_it_cannot_prove(pmm, knobs, metric, monkeypatch):
     assert np.array_equal(fsc.view(np.uint32), wsc.view(np.uint32))
 
 
-def test_bf16_ff_device_api_whole_problem(pmm, monkeypatch):
+def test_bf16_ff_device_api_whole_problem(pmm, ffn, monkeypatch):
     # the device entry point at a size with several splits per query block:
     # every row vs float64 truth on device, indices distinct
     import torch
 
     monkeypatch.setenv("PMM_BF16_FF", "1")
-    n = _native()
+    n = ffn
     dev = torch.device("cuda:0")
     g = torch.Generator(device=dev)
     g.manual_seed(37)

@@ -61,10 +61,32 @@ def test_oracle_similarity_kat(case):
 
 
 @pytest.mark.parametrize("case", [c for c in load_kats() if c["op"] == "select"], ids=lambda c: c["name"])
-def test_oracle_select_kat(case):
+@pytest.mark.parametrize("algo", ["total", "rust"])
+def test_oracle_select_kat(case, algo):
+    # the Rust-select restatement (the CPU baseline's select) must pass the
+    # reference's own select KATs too (src/topk.rs:83-125: no ties there)
     for dt in (np.float32, np.float64):
-        idx, _ = oracle.select_topk(np.array(case["s"], dtype=dt), case["k"], case["higher_is_better"])
+        idx, _ = oracle.select_topk(np.array(case["s"], dtype=dt), case["k"], case["higher_is_better"], algo=algo)
         assert idx.tolist() == case["expect_idx"]
+
+
+@pytest.mark.parametrize("m,n,k", [(40, 10000, 10), (20, 1000, 1), (20, 1000, 1000), (30, 5000, 100),
+                                   (5, 17, 16), (5, 17, 17), (7, 3, 2), (3, 100000, 100)])
+def test_rust_select_equals_checker_select(m, n, k):
+    # the baseline's select (Rust's select_nth_unstable_by
+    # + stable sort_by, restated in pmm_oracle.c) keeps the same k best scores
+    # in the same order as the checker's total-order select; only the order of
+    # equal scores may differ (unspecified in the reference, src/topk.rs:55-59)
+    rs = np.random.RandomState(m + n + k)
+    for dt in (np.float32, np.float64):
+        s = rs.randn(m, n).astype(dt)
+        s[:, ::7] = s[:, :1]  # runs of equal scores (the equal-pivot path)
+        for hib in (True, False):
+            i1, s1 = oracle.select_topk(s, k, hib)
+            i2, s2 = oracle.select_topk(s, k, hib, algo="rust")
+            assert np.array_equal(s1, s2), (dt, hib)
+            assert np.array_equal(np.take_along_axis(s, i2.astype(np.int64), 1), s2)
+            assert all(len(set(r)) == k for r in i2.tolist())
 
 
 def test_oracle_metric_parse():
