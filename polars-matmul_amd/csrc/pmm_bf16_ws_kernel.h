@@ -119,8 +119,14 @@ constexpr int drain_tiles() { return KS == 1 ? (PMM_WS_DRAIN_TILES < 2 ? PMM_WS_
 #endif
 #ifndef PMM_WS_QPS
 // 1: survivors queued by a per-group wave prefix sum of the lanes' counts
-// (see the epilogue); 0: one ballot round per survivor per lane (round 4)
-#define PMM_WS_QPS 1
+// (see the epilogue); 0 (default): one ballot round per survivor per lane.
+// Measured at c4 (round 5, lab builds alternated twice on one box,
+// profiles/r5_c4/qps_ab.txt): 173.3 / 173.4 ms per launch against 137.3 /
+// 137.4.  The sixteen per-score appends compile to sixteen VALU compare ->
+// exec mask -> branch chains per group (the pattern round 4 measured in
+// another form), while a group's survivors are few: the ballot loop runs
+// one or two rounds.  Kept as an A/B switch (make lab LAB=-DPMM_WS_QPS=1).
+#define PMM_WS_QPS 0
 #endif
 #ifndef PMM_WS_MFMA16
 // 1: the MFMA waves (and the seed) on v_mfma_f32_16x16x32_bf16 (default);
