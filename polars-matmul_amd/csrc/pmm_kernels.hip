@@ -1076,6 +1076,8 @@ struct PrologueArgs {
   unsigned sblocks, qblocks, cblocks, zblocks;
   int lds_seed;                // LDS-staged seed blocks (seed_lds_block)
   int64_t cper;                // LDS-staged launch: corpus norm rows per block
+  int ablate;                  // lab build only (PMM_PROLOGUE_ABLATE): 1 no seed blocks' work,
+                               // 2 seed without the k-th selection, 4 no norm / fill blocks' work
 };
 
 // LDS-staged seed block (ns <= 256 sample columns, padded D <= 1024): the
@@ -1260,6 +1262,7 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     return;
   }
   if (b >= a.sblocks) {
+    if (PMM_ABL(a.ablate & 4)) return;  // (lab: phase removal, results wrong)
     b -= a.sblocks;
     if (b < a.qblocks) {
       norms_rows<float, float>(a.q, a.m, a.d, a.ldq, a.squared, a.qn, nullptr, (int64_t)b * 256 + tid);
@@ -1278,6 +1281,7 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     }
     return;
   }
+  if (PMM_ABL(a.ablate & 1)) return;  // (lab: phase removal, results wrong)
   constexpr bool XFORM = METRIC != kMetricDot;
   const int dp = a.dp, d = a.d, ns = a.ns, m = a.m;
   u64 *keys = (u64 *)smem;                        // [RQ][64 E]
@@ -1369,6 +1373,13 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
   u64 x[E];
 #pragma unroll
   for (int e = 0; e < E; e++) x[e] = keys[w * 64 * E + lane + 64 * e];
+  if (PMM_ABL(a.ablate & 2)) {  // (lab: no selection; the keys stay live)
+    u64 t = 0ull;
+#pragma unroll
+    for (int e = 0; e < E; e++) t ^= x[e];
+    if (lane == 0) a.gthr[row] = (t == 0x0123456789abcdefull) ? t : 0ull;
+    return;
+  }
   const u64 th = wave_kth_u64<E>(x, a.k);  // nonzero: ns >= k keys, none of them 0
   if (lane == 0) a.gthr[row] = th ? th - 1 : 0ull;
 }
@@ -1441,6 +1452,9 @@ hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const floa
   // they apply.  A/B on one box, two alternations (profiles/r4_seed/): c1 step
   // 0.104 ms with the LDS-staged blocks against 0.099 ms (prologue 24 vs
   // 20 us), c2 0.096 vs 0.095 ms; bit-identical either way.
+#ifdef PMM_LAB
+  a.ablate = getenv("PMM_PROLOGUE_ABLATE") ? atoi(getenv("PMM_PROLOGUE_ABLATE")) : 0;
+#endif
   const char *le = getenv("PMM_SEED_LDS");
   a.lds_seed = (ns <= 256 && dp <= seedk::kLdsMaxDp && le && atoi(le) == 1) ? 1 : 0;
   a.sblocks = (unsigned)((m + seedk::RQ - 1) / seedk::RQ);

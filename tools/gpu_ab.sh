@@ -27,7 +27,7 @@ import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = d["roofline"]
 print(f"{sys.argv[2]:40s} run {sys.argv[3]}: step {d['ms_per_step']} ms, kernel {r['kernel_ms_avg']} ms, "
-      f"frac {r['frac']}, seed {r.get('seed_ms_avg')} ms")
+      f"frac {r['frac']}, seed/prologue {r.get('seed_ms_avg')} ms, merge {r.get('merge_ms_avg')} ms")
 EOF
   done
 done
