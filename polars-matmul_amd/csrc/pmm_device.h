@@ -137,6 +137,68 @@ __device__ inline u64 wave_kth_u64(const u64 (&x)[E], int k) {
     if (x[e] >= v && x[e] < t) t = x[e];
   return wave_min_u64(t);
 }
+// The same selection over 32-bit keys (0 = empty): the largest v with
+// #{x >= v} >= k, i.e. the k-th largest key (ties allowed).  Half the compare
+// work of the 64-bit form; the threshold seeds use it on the score part of
+// their composite keys (a lower bound of the composite k-th is all they need).
+template <int E>
+__device__ inline uint32_t wave_kth_u32(const uint32_t (&x)[E], int k) {
+  uint32_t mx = 0u, mn = ~0u;
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    mx = x[e] > mx ? x[e] : mx;
+    if (x[e] != 0u && x[e] < mn) mn = x[e];
+  }
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const uint32_t a = __shfl_xor(mx, o), c = __shfl_xor(mn, o);
+    mx = a > mx ? a : mx;
+    mn = c < mn ? c : mn;
+  }
+  if (mx == 0u) return 0u;
+  const uint32_t diff = mx ^ mn;
+  int b = diff ? 31 - __builtin_clz(diff) : -1;
+  uint32_t v = (b >= 0) ? (mx & ~((2u << b) - 1u)) : mx;  // (b = 31: 2u << 31 wraps to 0, v = 0)
+  for (; b >= 0; b--) {
+    const uint32_t c = v | (1u << b);
+    int cnt = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) cnt += __popcll(__ballot(x[e] >= c));
+    if (cnt >= k) {
+      v = c;
+      if (cnt == k) break;
+    }
+  }
+  uint32_t t = ~0u;
+#pragma unroll
+  for (int e = 0; e < E; e++)
+    if (x[e] >= v && x[e] < t) t = x[e];
+#pragma unroll
+  for (int o = 32; o; o >>= 1) {
+    const uint32_t a = __shfl_xor(t, o);
+    t = a < t ? a : t;
+  }
+  return t;
+}
+// Seeded threshold from the score part of a row's sample keys: every key
+// whose score key is at least the k-th largest passes ((kth << 32) - 1 is
+// below each of them, whatever its index part), so it is an exact lower bound
+// of the row's final k-th composite.  0 (accept all) when the sample has fewer
+// than k scores that are not NaN.
+template <int E>
+__device__ __forceinline__ u64 seed_threshold(const u64 (&x)[E], int k) {
+  uint32_t h[E];
+  int nz = 0;
+#pragma unroll
+  for (int e = 0; e < E; e++) {
+    h[e] = (uint32_t)(x[e] >> 32);
+    nz += __popcll(__ballot(h[e] != 0u));
+  }
+  if (nz < k) return 0ull;
+  const uint32_t t = wave_kth_u32<E>(h, k);
+  return t ? ((u64)t << 32) - 1ull : 0ull;
+}
+
 // Store the non-empty keys >= t of x packed (lane order) through st(pos, key);
 // returns their count.
 template <int E, typename Store>

@@ -1059,7 +1059,14 @@ hipError_t launch_seed_select(const float *S, int64_t lds, int m, int ns, int k,
 // coalesced loads measured slower (87 us: its load and compute phases
 // serialise), as did batching each lane's loads 8 deep (39 us against 28).
 namespace seedk {
-constexpr int RQ = 4;  // query rows per seed block (one per wave for the selection)
+#ifndef PMM_SEED_RQ
+#define PMM_SEED_RQ 4
+#endif
+// query rows per seed block (a multiple of 4: the block's 4 waves select RQ / 4
+// rows each).  Every lane streams its sample column's row once per block, so
+// RQ rows share each corpus load.
+constexpr int RQ = PMM_SEED_RQ;
+static_assert(RQ % 4 == 0 && RQ <= 16, "seed rows per block");
 }  // namespace seedk
 struct PrologueArgs {
   const float *q;
@@ -1078,6 +1085,7 @@ struct PrologueArgs {
   int64_t cper;                // LDS-staged launch: corpus norm rows per block
   int ablate;                  // lab build only (PMM_PROLOGUE_ABLATE): 1 no seed blocks' work,
                                // 2 seed without the k-th selection, 4 no norm / fill blocks' work
+  int mfma_seed;               // seed blocks on v_mfma_f32_16x16x4_f32 (prologue_mfma_kernel)
 };
 
 // LDS-staged seed block (ns <= 256 sample columns, padded D <= 1024): the
@@ -1162,7 +1170,7 @@ __device__ __forceinline__ void seed_lds_block(const PrologueArgs &a, unsigned b
       if (on) *(f32x4 *)(qs + r * dp + 4 * tid) = v[r];
   }
   __syncthreads();
-  if (XFORM && w == 0) norms_rows<float, float>(qs, RQ, d, dp, a.squared, qn_s, nullptr, tid);
+  if (XFORM && w < (RQ + 7) / 8) norms_rows<float, float>(qs, RQ, d, dp, a.squared, qn_s, nullptr, tid);
   __syncthreads();
   const int col = tid, d8 = d & ~7;
   float acc[RQ];
@@ -1225,13 +1233,15 @@ __device__ __forceinline__ void seed_lds_block(const PrologueArgs &a, unsigned b
   }
   __syncthreads();
   if (XFORM && tid < RQ && row0 + tid < m) a.qn[row0 + tid] = qn_s[tid];
-  const int row = row0 + w;
-  if (row >= m) return;
-  u64 x[4];
+  for (int rr = w; rr < RQ; rr += 4) {
+    const int row = row0 + rr;
+    if (row >= m) return;
+    u64 x[4];
 #pragma unroll
-  for (int e = 0; e < 4; e++) x[e] = keys[w * 256 + lane + 64 * e];
-  const u64 th = wave_kth_u64<4>(x, a.k);  // nonzero: ns >= k keys, none of them 0
-  if (lane == 0) a.gthr[row] = th ? th - 1 : 0ull;
+    for (int e = 0; e < 4; e++) x[e] = keys[rr * 256 + lane + 64 * e];
+    const u64 th = seed_threshold<4>(x, a.k);  // a lower bound of the row's final k-th
+    if (lane == 0) a.gthr[row] = th;
+  }
 }
 
 template <int E, int METRIC, int LDSK>
@@ -1295,7 +1305,7 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
       *(f32x4 *)(qs + r * dp + 4 * j4) = v;
     }
   __syncthreads();
-  if (XFORM && w == 0) norms_rows<float, float>(qs, RQ, d, dp, a.squared, qn_s, nullptr, tid);
+  if (XFORM && w < (RQ + 7) / 8) norms_rows<float, float>(qs, RQ, d, dp, a.squared, qn_s, nullptr, tid);
   __syncthreads();
   const int d8 = d & ~7;
   for (int col = tid; col < 64 * E; col += 256) {
@@ -1368,20 +1378,242 @@ __global__ __launch_bounds__(256) void prologue_kernel(PrologueArgs a) {
     }
   }
   __syncthreads();
-  const int row = row0 + w;
-  if (row >= m) return;
-  u64 x[E];
+  for (int rr = w; rr < RQ; rr += 4) {
+    const int row = row0 + rr;
+    if (row >= m) return;
+    u64 x[E];
 #pragma unroll
-  for (int e = 0; e < E; e++) x[e] = keys[w * 64 * E + lane + 64 * e];
-  if (PMM_ABL(a.ablate & 2)) {  // (lab: no selection; the keys stay live)
-    u64 t = 0ull;
+    for (int e = 0; e < E; e++) x[e] = keys[rr * 64 * E + lane + 64 * e];
+    if (PMM_ABL(a.ablate & 2)) {  // (lab: no selection; the keys stay live)
+      u64 t = 0ull;
 #pragma unroll
-    for (int e = 0; e < E; e++) t ^= x[e];
-    if (lane == 0) a.gthr[row] = (t == 0x0123456789abcdefull) ? t : 0ull;
+      for (int e = 0; e < E; e++) t ^= x[e];
+      if (lane == 0) a.gthr[row] = (t == 0x0123456789abcdefull) ? t : 0ull;
+      continue;
+    }
+    const u64 th = seed_threshold<E>(x, a.k);  // a lower bound of the row's final k-th
+    if (lane == 0) a.gthr[row] = th;
+  }
+}
+
+// ===========================================================================
+// The prologue with MFMA seed blocks (ns = 256 sample columns, padded D <=
+// 1024).  The row-streaming seed block above spends ~13 of the c1
+// prologue's ~17 us streaming each lane's own 1 KiB sample row (every load
+// instruction touches 64 rows) for 4 query rows at a time.  Here a seed block
+// takes 16 query rows and the whole sample on v_mfma_f32_16x16x4_f32: each
+// MFMA is bitwise a k-ordered fmaf chain over its 4 k (MI355X_MICROARCH.md,
+// FP32-input MFMA), and step s feeds k = 4s + (lane >> 4), so every score is
+// the chain over k = 0 .. dp-1 in natural order -- the main pass's and the
+// fmaf-chain seed block's value, bit for bit.  The sample streams through LDS
+// in K chunks of 32 floats (8 threads per column row piece: 128-byte runs),
+// double-buffered, one barrier per chunk; the query rows stay in LDS.  8
+// waves, 32 sample columns each (two accumulator chains per wave: the
+// 16x16x4's dependent latency is 40 cycles against a 32-cycle issue).  The
+// sample columns' norms come from the same chunks in ndarray order (thread c
+// owns column c's 8 partial sums), the query rows' from the staged rows.
+// Other block kinds (query / corpus norms, fills) as in prologue_kernel, at
+// 512 threads per block.
+// ===========================================================================
+namespace seedm {
+constexpr int RM = 16;          // query rows per seed block (the MFMA's M)
+#ifndef PMM_SEEDM_NT
+#define PMM_SEEDM_NT 1024
+#endif
+constexpr int NT = PMM_SEEDM_NT;  // threads per block: 16 waves, one query row each for the selection
+constexpr int NCH = 256 / (NT / 64) / 16;  // 16-column accumulator chains per wave
+constexpr int NSM = 256;        // sample columns
+constexpr int KC = 32;          // K floats per corpus chunk
+constexpr int CS = KC + 4;      // LDS row stride of a chunk (floats): conflict-free B reads
+constexpr int kMaxDp = 1024;
+__host__ __device__ constexpr size_t lds_bytes(int dp) {
+  return (size_t)RM * (dp + 4) * 4 + (size_t)2 * NSM * CS * 4 + RM * 4 + NSM * 4;
+}
+static_assert((size_t)RM * NSM * 8 <= (size_t)2 * NSM * CS * 4, "keys alias the chunk buffers");
+}  // namespace seedm
+
+template <int METRIC>
+__device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned b, char *smem) {
+  using namespace seedm;
+  constexpr bool XFORM = METRIC != kMetricDot;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int dp = a.dp, d = a.d, m = a.m;
+  const int QS = dp + 4;                 // query row stride in LDS: conflict-free A reads
+  float *qs = (float *)smem;             // [RM][QS]
+  float *cbuf = qs + RM * QS;            // [2][NSM][CS]
+  float *qn_s = cbuf + 2 * NSM * CS;     // [RM]
+  float *cn_s = qn_s + RM;               // [NSM]
+  u64 *keys = (u64 *)cbuf;               // [RM][NSM], after the K loop
+  const int row0 = (int)b * RM;
+  const int G = dp / KC;
+  // the corpus chunk's pieces of this thread: piece p = tid + NT u -> column
+  // p >> 3, 16-byte part p & 7 (8 consecutive threads read one 128-byte run).
+  // Chunks stream through PFC register sets: chunk t + PFC - 1's loads are
+  // issued while chunk t is computed (with one set, each chunk's L2 / HBM
+  // latency was exposed: the MFMA blocks took as long as the fmaf-chain ones)
+  constexpr int PFC = 4;
+  constexpr int NPC = NSM * 8 / NT;  // 16-byte pieces per thread per chunk
+  f32x4 v[PFC][NPC];
+  auto load_chunk = [&](int t, f32x4 (&r)[NPC]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NPC; u++) {
+      const int pc = tid + NT * u, col = pc >> 3, part = pc & 7;
+      r[u] = *(const f32x4 *)(a.c + (int64_t)col * a.ldc + t * KC + 4 * part);
+    }
+  };
+  auto store_chunk = [&](int buf, const f32x4 (&r)[NPC]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < NPC; u++) {
+      const int pc = tid + NT * u, col = pc >> 3, part = pc & 7;
+      *(f32x4 *)(cbuf + buf * NSM * CS + col * CS + 4 * part) = r[u];
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < PFC; j++) load_chunk(min(j, G - 1), v[j]);  // (clamped: every load unconditional)
+  for (int i = tid; i < RM * (dp / 4); i += NT) {
+    const int r = i / (dp / 4), j4 = i - r * (dp / 4);
+    f32x4 x = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (row0 + r < m) x = *(const f32x4 *)(a.q + (int64_t)(row0 + r) * a.ldq + 4 * j4);
+    *(f32x4 *)(qs + r * QS + 4 * j4) = x;
+  }
+  store_chunk(0, v[0]);
+  __syncthreads();
+  const int g4 = lane >> 4, l16 = lane & 15;
+  const int col0 = 16 * NCH * w + l16;  // chain c: column col0 + 16 c
+  const int d8 = d & ~7;
+  f32x4 acc[NCH];
+#pragma unroll
+  for (int c = 0; c < NCH; c++) acc[c] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  float p[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) p[j] = 0.0f;
+  // (every load and LDS store unconditional, past the last chunk on clamped
+  // or unused data: the compiler then counts the loads in flight instead of
+  // waiting for all of them at each branch)
+  for (int t0 = 0; t0 < (PMM_ABL(a.ablate & 8) ? 0 : G); t0 += PFC) {  // (lab 8: no K loop)
+#pragma unroll
+    for (int j = 0; j < PFC; j++) {
+      const int t = t0 + j;
+      if (t < G) {
+      const float *cb = cbuf + (t & 1) * NSM * CS;
+      const float *qa = qs + l16 * QS + t * KC + g4;
+#pragma unroll
+      for (int s4 = 0; s4 < KC / 4; s4++) {
+        const float av = qa[4 * s4];
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+          acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, cb[(col0 + 16 * c) * CS + 4 * s4 + g4], acc[c], 0, 0, 0);
+      }
+      if (XFORM && tid < NSM) {
+        // column tid's norm partials in ndarray order: accumulator j sums
+        // x[8t + j]^2 over t (the chunk's float4 j4 holds k = 4 j4 .. 4 j4 + 3)
+        const float *cc = cb + tid * CS;
+#pragma unroll
+        for (int j4 = 0; j4 < KC / 4; j4++) {
+          if (t * KC + 4 * j4 < d8) {
+            const f32x4 x = *(const f32x4 *)(cc + 4 * j4);
+            const int o = (j4 & 1) * 4;
+#pragma unroll
+            for (int e = 0; e < 4; e++) p[o + e] = p[o + e] + x[e] * x[e];
+          }
+        }
+      }
+      }
+      // chunk t + 1 into the other buffer (its last readers, chunk t - 1,
+      // passed the previous barrier); chunk t + PFC into chunk t's registers
+      store_chunk((t + 1) & 1, v[(j + 1) % PFC]);
+      load_chunk(min(t + PFC, G - 1), v[j]);
+      __syncthreads();
+    }
+  }
+  if (XFORM && tid < NSM) {
+    float sum = 0.0f;
+    sum = sum + (p[0] + p[4]);
+    sum = sum + (p[1] + p[5]);
+    sum = sum + (p[2] + p[6]);
+    sum = sum + (p[3] + p[7]);
+    const float *crow = a.c + (int64_t)tid * a.ldc;
+    for (int i = d8; i < d; i++) {
+      const float x = crow[i];
+      sum = sum + x * x;
+    }
+    cn_s[tid] = a.squared ? sum : sqrt_rn<float>(sum);
+  }
+  if (XFORM && w < RM / 8) norms_rows<float, float>(qs, RM, d, QS, a.squared, qn_s, nullptr, tid);
+  __syncthreads();
+  // D of the 16x16x4: lane holds rows 4 (lane >> 4) + i of its column
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int r = 4 * g4 + i;
+    const bool ok = row0 + r < m;
+    const float qv = XFORM ? qn_s[r] : 0.0f;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+      const int col = col0 + 16 * c;
+      const float sc = exact_score<METRIC>(acc[c][i], qv, XFORM ? cn_s[col] : 0.0f);
+      keys[r * NSM + col] =
+          ok ? (((u64)okey32(METRIC == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~(uint32_t)col)) : 0ull;
+    }
+  }
+  __syncthreads();
+  for (int rr = w; rr < RM; rr += NT / 64) {
+    const int row = row0 + rr;
+    if (row >= m) return;
+    u64 x[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) x[e] = keys[rr * NSM + lane + 64 * e];
+    if (PMM_ABL(a.ablate & 16)) {  // (lab: no selection; the keys stay live)
+      u64 t = 0ull;
+#pragma unroll
+      for (int e = 0; e < 4; e++) t ^= x[e];
+      if (lane == 0) a.gthr[row] = (t == 0x0123456789abcdefull) ? t : 0ull;
+      continue;
+    }
+    const u64 th = seed_threshold<4>(x, a.k);  // a lower bound of the row's final k-th
+    if (lane == 0) a.gthr[row] = th;
+  }
+}
+
+template <int METRIC>
+__global__ __launch_bounds__(seedm::NT) void prologue_mfma_kernel(PrologueArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x;
+  unsigned b = blockIdx.x;
+  if (b < a.sblocks) {
+    if (PMM_ABL(a.ablate & 1)) return;  // (lab: phase removal, results wrong)
+    seed_mfma_block<METRIC>(a, b, smem);
     return;
   }
-  const u64 th = wave_kth_u64<E>(x, a.k);  // nonzero: ns >= k keys, none of them 0
-  if (lane == 0) a.gthr[row] = th ? th - 1 : 0ull;
+  if (PMM_ABL(a.ablate & 4)) return;
+  b -= a.sblocks;
+  if (b < a.qblocks) {
+    norms_rows<float, float>(a.q, a.m, a.d, a.ldq, a.squared, a.qn, nullptr, (int64_t)b * seedm::NT + tid);
+    return;
+  }
+  b -= a.qblocks;
+  if (b < a.cblocks) {
+    norms_rows<float, float>(a.c, a.n, a.d, a.ldc, a.squared, a.cn, a.cinv, (int64_t)b * seedm::NT + tid);
+    return;
+  }
+  b -= a.cblocks;
+  const int64_t stride = (int64_t)a.zblocks * seedm::NT;
+  for (int64_t i = (int64_t)b * seedm::NT + tid; i < a.z0n + a.z1n; i += stride) {
+    if (i < a.z0n) a.z0[i] = make_uint4(0u, 0u, 0u, 0u);
+    else a.z1[i - a.z0n] = make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
+template <int METRIC>
+static hipError_t launch_prologue_mfma_t(const PrologueArgs &a, unsigned grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute((const void *)prologue_mfma_kernel<METRIC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  prologue_mfma_kernel<METRIC><<<grid, seedm::NT, seedm::lds_bytes(a.dp), s>>>(a);
+  return hipGetLastError();
 }
 
 template <int METRIC, int LDSK>
@@ -1416,6 +1648,11 @@ static hipError_t launch_prologue_t(const PrologueArgs &a, unsigned grid, hipStr
   return a.lds_seed ? launch_prologue_t2<METRIC, 1>(a, grid, s) : launch_prologue_t2<METRIC, 0>(a, grid, s);
 }
 
+#ifndef PMM_SEED_MFMA_DEFAULT
+// MFMA seed blocks by default: c1 step 0.099 vs 0.100 ms, prologue 18 vs
+// 19-20 us (bench events), c2 0.096 vs 0.097 (profiles/r5_c1/seed_ab.txt)
+#define PMM_SEED_MFMA_DEFAULT 1
+#endif
 hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const float *c, int64_t ldc, int64_t n,
                                   int d, int dp, int ns, int k, int metric, float *qn, float *cn, bool corpus_norms,
                                   unsigned long long *gthr, void *z0, size_t z0_bytes, void *z1, size_t z1_bytes,
@@ -1457,8 +1694,24 @@ hipError_t launch_seeded_prologue(const float *q, int64_t ldq, int m, const floa
 #endif
   const char *le = getenv("PMM_SEED_LDS");
   a.lds_seed = (ns <= 256 && dp <= seedk::kLdsMaxDp && le && atoi(le) == 1) ? 1 : 0;
-  a.sblocks = (unsigned)((m + seedk::RQ - 1) / seedk::RQ);
   const bool xf = metric != kMetricDot;
+  // MFMA seed blocks (prologue_mfma_kernel) for a 256-column sample; PMM_SEED_MFMA
+  // (read per call) 0 / 1 forces the fmaf-chain blocks / the MFMA blocks
+  const char *me = getenv("PMM_SEED_MFMA");
+  const bool mfma_ok = ns == seedm::NSM && dp <= seedm::kMaxDp && !a.lds_seed && n >= seedm::NSM;
+  a.mfma_seed = (mfma_ok && (me ? atoi(me) != 0 : PMM_SEED_MFMA_DEFAULT != 0)) ? 1 : 0;
+  if (a.mfma_seed) {
+    a.sblocks = (unsigned)((m + seedm::RM - 1) / seedm::RM);
+    constexpr int T = seedm::NT;
+    a.qblocks = xf ? (unsigned)((m * 8 + T - 1) / T) : 0u;
+    a.cblocks = (xf && corpus_norms) ? (unsigned)((n * 8 + T - 1) / T) : 0u;
+    a.zblocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((a.z0n + a.z1n + T - 1) / T, 16));
+    const unsigned grid = a.sblocks + a.qblocks + a.cblocks + a.zblocks;
+    if (metric == kMetricCosine) return launch_prologue_mfma_t<kMetricCosine>(a, grid, s);
+    if (metric == kMetricDot) return launch_prologue_mfma_t<kMetricDot>(a, grid, s);
+    return launch_prologue_mfma_t<kMetricEuclidean>(a, grid, s);
+  }
+  a.sblocks = (unsigned)((m + seedk::RQ - 1) / seedk::RQ);
   unsigned grid;
   if (a.lds_seed) {
     // one block kind: seed blocks, plus norms-only blocks so that no block

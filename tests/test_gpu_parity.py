@@ -1058,8 +1058,13 @@ def test_threshold_seeding_changes_nothing(pmm, k, d, monkeypatch):
         monkeypatch.setenv("PMM_SEED_LDS", "1")  # the LDS-staged seed blocks (opt-in)
         got_f = gpu_topk(q, c, k, metric)
         monkeypatch.delenv("PMM_SEED_LDS")
+        outs = [got, got_g, got_f]
+        for mf in ("0", "1"):  # fmaf-chain seed blocks / MFMA seed blocks (ns = 256 only)
+            monkeypatch.setenv("PMM_SEED_MFMA", mf)
+            outs.append(gpu_topk(q, c, k, metric))
+        monkeypatch.delenv("PMM_SEED_MFMA")
         monkeypatch.delenv("PMM_SEED")
-        for g in (got, got_g, got_f):
+        for g in outs:
             assert np.array_equal(g[0], want[0]), metric
             assert np.array_equal(g[1], want[1]), metric
         check_topk(got[0], got[1], truth_scores(q, c, metric), metric != "euclidean",
@@ -1067,9 +1072,9 @@ def test_threshold_seeding_changes_nothing(pmm, k, d, monkeypatch):
 
 
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-@pytest.mark.parametrize("seed_lds", ["1", "0"])
-@pytest.mark.parametrize("d", [256, 96, 37])
-def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, seed_lds, d, monkeypatch):
+@pytest.mark.parametrize("seed_mode", ["lds", "rows", "mfma"])
+@pytest.mark.parametrize("d", [256, 96, 37, 1000])
+def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, seed_mode, d, monkeypatch):
     # Every row's true top-k lies inside the seed sample (the corpus's first
     # ns = 256 rows hold 16 near-copies of each query).  The seed's threshold
     # is (the sample's k-th composite) - 1, so if the seed scored the k-th
@@ -1082,12 +1087,15 @@ def test_seed_scores_equal_main_pass_when_topk_is_in_the_sample(pmm, metric, see
     q = rs.randn(m, d).astype(np.float32)
     c = (rs.randn(N, d) * 0.3).astype(np.float32)
     c[:256] = q[np.arange(256) % m] + 0.05 * rs.randn(256, d).astype(np.float32)
+    # (the seed blocks: LDS-staged fmaf chains, row-streaming fmaf chains, or
+    # v_mfma_f32_16x16x4_f32 chains)
     monkeypatch.setenv("PMM_SEED", "1")
-    monkeypatch.setenv("PMM_SEED_LDS", seed_lds)
+    monkeypatch.setenv("PMM_SEED_LDS", "1" if seed_mode == "lds" else "0")
+    monkeypatch.setenv("PMM_SEED_MFMA", "1" if seed_mode == "mfma" else "0")
     idx, sc = gpu_topk(q, c, k, metric)
     assert int(idx.max()) < 256  # the top-k really is inside the sample
     oi, osc = oracle.topk(q, c, k, METRICS[metric])
-    assert_bitexact(idx, sc, oi, osc, f"seed-sample top-k {metric} lds={seed_lds}")
+    assert_bitexact(idx, sc, oi, osc, f"seed-sample top-k {metric} {seed_mode}")
 
 
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
