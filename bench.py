@@ -1239,7 +1239,17 @@ def main():
     import torch
 
     dist = None
-    if world > 1:
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0 and
+    # the gloo backend (RCCL refuses two ranks on one GPU); the numbers of such
+    # a run measure nothing, the line says so
+    share = world > 1 and os.environ.get("PMM_BENCH_SHARE_GPU") == "1"
+    if share:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+        os.environ.setdefault("PMM_BENCH_INPROC_DEVICES", ",".join("0" * world))
+    elif world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
@@ -1354,6 +1364,8 @@ def main():
         "extra": extra if inproc is None else dict(extra or {}, inproc=inproc),
         "check": fields["check"],
     }
+    if share:
+        line["rehearsal"] = "PMM_BENCH_SHARE_GPU=1: every rank on device 0, gloo; not a measurement"
     line["summary"] = summary_of(line)  # (last key: see summary_of)
     if spawner:
         spawner.close()
