@@ -1050,6 +1050,13 @@ int validate_sizes(int64_t m, int64_t n, int64_t d, int64_t k, bool topk, bool a
   return PMM_OK;
 }
 
+// A non-empty call needs every buffer it names (the reference never passes
+// null; a binding that does gets an error instead of a fault).
+template <typename... P>
+int need_buffers(P... p) {
+  return ((p != nullptr) && ...) ? PMM_OK : fail(PMM_ERR_ARG, "null argument");
+}
+
 // Host-buffer f32 top-k over a large corpus with the upload overlapped with
 // compute.  The corpus is cut into chunks: a small first one (uploaded, with
 // the queries, before any compute) and CHUNKS-1 equal ones.  Chunk i + 1 is
@@ -1821,6 +1828,7 @@ int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, 
     return fail(PMM_ERR_UNSUPPORTED, "unknown compute mode %d", compute);
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
+  if ((rc = need_buffers(q, c, out_idx, out_score))) return rc;
   const int64_t dp = cdiv(d, 32) * 32;
   if (d == 0 || ldq % 4 != 0 || ldc % 4 != 0 || ldq < dp || ldc < dp || ((uintptr_t)q & 15) ||
       ((uintptr_t)c & 15))
@@ -1845,6 +1853,7 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  if ((rc = need_buffers(q, c, out_idx, out_score))) return rc;
   if (compute == PMM_COMPUTE_BF16 && (rc = bf16_limits(d, k, n))) return rc;
   {
     // a device list (pmm_set_devices): the corpus row-sharded over it, one
@@ -1929,6 +1938,7 @@ int pmm_topk_bf16_device(const uint16_t *q, int64_t ldq, int64_t m, const uint16
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  if ((rc = need_buffers(q, c, out_idx, out_score))) return rc;
   if ((rc = bf16_limits(d, k, n))) return rc;
   const int64_t dp = cdiv(d, kBf16DAlign) * kBf16DAlign;
   if (ldq % 8 != 0 || ldc % 8 != 0 || ldq < dp || ldc < dp || ((uintptr_t)q & 15) ||
@@ -1957,6 +1967,7 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  if ((rc = need_buffers(q, c, out_idx, out_score))) return rc;
   int dev;
   DevScope scope;
   if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
@@ -1992,6 +2003,7 @@ int pmm_topk_f64_device(const double *q, int64_t ldq, int64_t m, const double *c
   if ((rc = check_metric(metric))) return rc;
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
+  if ((rc = need_buffers(q, c, out_idx, out_score))) return rc;
   const int64_t dp = cdiv(d, 16) * 16;
   if (d == 0 || ldq < dp || ldc < dp || ((uintptr_t)q & 15) || ((uintptr_t)c & 15))
     return fail(PMM_ERR_ARG,
@@ -2013,6 +2025,7 @@ int pmm_matmul_f32(const float *q, int64_t m, const float *c, int64_t n, int64_t
   int rc = validate_sizes(m, n, d, 0, false);
   if (rc) return rc;
   if (m == 0 || n == 0) return PMM_OK;
+  if ((rc = need_buffers(q, c, out))) return rc;
   int dev;
   DevScope scope;
   if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
@@ -2047,6 +2060,7 @@ int pmm_matmul_f64(const double *q, int64_t m, const double *c, int64_t n, int64
   int rc = validate_sizes(m, n, d, 0, false);
   if (rc) return rc;
   if (m == 0 || n == 0) return PMM_OK;
+  if ((rc = need_buffers(q, c, out))) return rc;
   int dev;
   DevScope scope;
   if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
@@ -2146,6 +2160,7 @@ int pmm_corpus_create_f32(const float *c, int64_t n, int64_t d, pmm_corpus **out
   if (rc) return rc;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
+  if (!c) return fail(PMM_ERR_ARG, "null argument");
   int dev;
   DevScope scope;
   if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
@@ -2287,6 +2302,7 @@ int pmm_topk_f64_corpus(const pmm_corpus *h, const double *q, int64_t m, int64_t
   if (rc) return rc;
   if ((rc = check_metric(metric))) return rc;
   if (m == 0 || k == 0) return PMM_OK;
+  if ((rc = need_buffers(q, out_idx, out_score))) return rc;
   const CorpusShard &x = h->shards[0];
   int dev;
   DevScope scope;
@@ -2325,6 +2341,7 @@ int pmm_topk_f32_corpus(const pmm_corpus *h, const float *q, int64_t m, int64_t 
   if (rc) return rc;
   if ((rc = check_metric(metric))) return rc;
   if (m == 0 || k == 0) return PMM_OK;
+  if ((rc = need_buffers(q, out_idx, out_score))) return rc;
   // which of a shard's norm arrays this metric reads (none for dot)
   auto shard_norms = [&](const CorpusShard &x) -> const float * {
     return metric == kMetricCosine ? x.norms : metric == kMetricEuclidean ? x.norms + 2 * x.n : nullptr;

@@ -190,6 +190,37 @@ def test_compute_fails_loudly_without_device():
         polars_matmul.matmul(np.ones((2, 2)), np.ones((2, 2)))
 
 
+def test_null_buffers_are_refused_before_any_device_call():
+    # a non-empty call with a null buffer is an argument error, not a fault;
+    # checked before the device is touched, so it runs here without a GPU
+    lib = _native.lib()
+    a = np.ones((4, 8), dtype=np.float32)
+    a64 = a.astype(np.float64)
+    oi = np.zeros(4, dtype=np.uint32)
+    os_ = np.zeros(4, dtype=np.float32)
+    os64 = np.zeros(4, dtype=np.float64)
+    P = lambda x: x.ctypes.data  # noqa: E731
+    calls = [
+        lambda: lib.pmm_topk_f32(None, 4, P(a), 4, 8, 1, 0, P(oi), P(os_)),
+        lambda: lib.pmm_topk_f32(P(a), 4, None, 4, 8, 1, 0, P(oi), P(os_)),
+        lambda: lib.pmm_topk_f32(P(a), 4, P(a), 4, 8, 1, 0, None, P(os_)),
+        lambda: lib.pmm_topk_f32(P(a), 4, P(a), 4, 8, 1, 0, P(oi), None),
+        lambda: lib.pmm_topk_f64(P(a64), 4, None, 4, 8, 1, 0, P(oi), P(os64)),
+        lambda: lib.pmm_topk_f64(P(a64), 4, P(a64), 4, 8, 1, 0, P(oi), None),
+        lambda: lib.pmm_matmul_f32(P(a), 4, P(a), 4, 8, None),
+        lambda: lib.pmm_matmul_f64(None, 4, P(a64), 4, 8, P(os64)),
+    ]
+    for call in calls:
+        assert call() == _native.PMM_ERR_ARG
+        assert _native.last_error() == "null argument"
+    h = ctypes.c_void_p()
+    assert lib.pmm_corpus_create_f32(None, 4, 8, ctypes.byref(h)) == _native.PMM_ERR_ARG
+    assert not h.value
+    # empty calls need no buffers (src/matmul.rs:480-487 returns before any work)
+    assert lib.pmm_topk_f32(None, 0, None, 4, 8, 1, 0, None, None) == 0
+    assert lib.pmm_matmul_f32(None, 0, None, 4, 8, None) == 0
+
+
 def test_pmm_namespace_placeholder_without_polars():
     try:
         import polars  # noqa: F401
