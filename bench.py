@@ -163,13 +163,16 @@ def ref_inputs(M, N, D):
     return q, c
 
 
+METRIC_OVERRIDE = None  # --metric: the main config's metric replaced (no traffic record applies)
+
+
 def load_traffic(config: str):
     """(HBM bytes per launch of the dominant kernel, its source record) from
     the committed rocprofv3 --pmc summary of this build (profiles/
     pmc_traffic_<config>.json, written by tools/traffic_json.py), corrected as
     MI355X_MICROARCH.md prescribes."""
     path = os.path.join(ROOT, "profiles", f"pmc_traffic_{config}.json")
-    if not os.path.exists(path):
+    if METRIC_OVERRIDE or not os.path.exists(path):  # the records are of the configs' own metric
         return None, None
     try:
         with open(path) as f:
@@ -1035,7 +1038,7 @@ def run_inproc_child(args, world, spawner):
            if kk not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
                          "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID")}
     cmd = [sys.executable, os.path.abspath(__file__), "--inproc-child", str(world), "--config", args.config,
-           "--steps", str(args.steps), "--warmup", str(args.warmup)]
+           "--steps", str(args.steps), "--warmup", str(args.warmup)] + (["--metric", args.metric] if args.metric else [])
     r = spawner.run(cmd, env, args.inproc_timeout)
     lines = [x for x in r["stdout"].splitlines() if x.startswith("{")]
     if r["rc"] != 0 or not lines:
@@ -1203,6 +1206,8 @@ def main():
                          "'matmul' = .pmm.matmul at the c1 size; 'c1_f64' = the f64 top-k at the c1 size; "
                          "'f64_large' = the f64 top-k at 4096 x 1M x 256; 'c5_rank' = configs[4]'s per-GPU "
                          "share, 1M x 1.25M x 1024, 1 warm-up + 2 timed steps)")
+    ap.add_argument("--metric", choices=("cosine", "dot", "euclidean"), default=None,
+                    help="replace the main config's metric (the extras keep theirs)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 top-k")
     ap.add_argument("--timing-stride", type=int, default=0,
                     help="record the per-kernel HIP events on every n-th timed step (0: every step of "
@@ -1214,6 +1219,10 @@ def main():
     ap.add_argument("--inproc-timeout", type=int, default=900, help=argparse.SUPPRESS)
     ap.add_argument("--inproc-child", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.metric and args.metric != CONFIGS[args.config][4]:
+        global METRIC_OVERRIDE
+        METRIC_OVERRIDE = args.metric
+        CONFIGS[args.config] = CONFIGS[args.config][:4] + (args.metric,) + CONFIGS[args.config][5:]
     if args.inproc_child:
         inproc_child(args)
         return
@@ -1339,7 +1348,7 @@ def main():
         log(f"inproc: {inproc}")
 
     line = {
-        "metric": "cosine top-k queries/sec",
+        "metric": f"{metric} top-k queries/sec",
         "value": fields["value"],
         "unit": "queries/s",
         "n_gpus": world,
