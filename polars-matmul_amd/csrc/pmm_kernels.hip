@@ -343,6 +343,15 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     // of the first two MFMA groups: c1 0.141 vs 0.143 ms, c2 0.134 vs 0.136;
     // 2 behind each of four groups 0.146 / 0.139)
     constexpr int NPART = (NB <= 4 && NW == 4) ? PMM_F32_DMA_PARTS_SMALL : PMM_F32_DMA_PARTS;
+// The large variants' pre-filter in two passes: per-lane survivor flags with
+// no branches, their OR over the wave, then ballot + append at the flagged
+// positions only (wave-uniform element index).  The one-pass form ran a
+// compare -> ballot -> branch chain per score (~50 cycles each, MFMA idle):
+// c3 1053.7 / 1055.1 vs 1063.1 / 1063.6 ms, alternated on one box
+// (profiles/r5_pf2/ab.txt); the queue order and so the results are unchanged.
+#ifndef PMM_F32_PF2
+#define PMM_F32_PF2 1
+#endif
 #ifndef PMM_F32_FRAG_PREFETCH
 #define PMM_F32_FRAG_PREFETCH 1  // (A/B: 0 off, 1 the 128 x 128 variant only, 2 every variant)
 #endif
@@ -575,6 +584,49 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           }
           qlen += tot;
         } else {
+#if PMM_F32_PF2
+          // pass 1, no branches: each lane's survivor flags (16 per column
+          // block c, two blocks per word), then their OR over the wave -- the
+          // positions (c, e) where some lane holds a survivor; only those
+          // take the ballot + append below
+          uint32_t fl[(NB + 1) / 2], U[(NB + 1) / 2];
+#pragma unroll
+          for (int i = 0; i < (NB + 1) / 2; i++) fl[i] = 0u;
+#pragma unroll
+          for (int c = 0; c < NB; c++) {
+            const float cv = XFORM ? cvt[32 * c + r32] : 0.0f;
+            uint32_t f = 0u;
+#pragma unroll
+            for (int e = 0; e < 16; e++) f |= (prefilter(acc[c][e], cv) < lo[e]) ? 0u : (1u << e);
+            if (col0 + 32 * c + r32 >= a.N) f = 0u;
+            fl[c >> 1] |= f << (16 * (c & 1));
+          }
+#pragma unroll
+          for (int i = 0; i < (NB + 1) / 2; i++) {
+            uint32_t x = fl[i];
+#pragma unroll
+            for (int off = 32; off; off >>= 1) x |= (uint32_t)__shfl_xor((int)x, off);
+            U[i] = __builtin_amdgcn_readfirstlane(x);
+          }
+          // pass 2: the flagged positions only, block by block (e is
+          // wave-uniform: the accumulator element is read by index)
+#pragma unroll
+          for (int c = 0; c < NB; c++) {
+            uint32_t uc = (U[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
+            while (uc) {
+              const int e = __builtin_ctz(uc);
+              uc &= uc - 1u;
+              const bool p = (fl[c >> 1] >> (16 * (c & 1) + e)) & 1u;
+              const u64 m = __ballot(p);
+              if (p && PMM_ABL(a.ablate) != 2) {
+                const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
+                gq[qlen + lanes_below(m)] = (u64)__float_as_uint(acc[c][e]) | ((u64)hi << 32);
+              }
+              qlen += __popcll(m);
+            }
+          }
+        }
+#else
 #pragma unroll
           for (int c = 0; c < NB; c++) {
             const int gcol = col0 + 32 * c + r32;
@@ -595,6 +647,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             }
           }
         }
+#endif
         if (PMM_ABL(a.ablate) == 2) qlen = 0;  // ablation: pre-filter only
         if (qlen) {
           // queue entries past the LDS part: their stores reached L2
