@@ -283,11 +283,9 @@ void plan_units(int64_t m, int64_t n, int bm, int bn, int cus, double unit_overh
 // Small problems (fewer than 4 x CUs 256 x 256 tiles: the reference's own
 // 1000 x 10000 benchmark size) fill the chip better with 128 x 128 tiles.
 int choose_variant(int mode, int capg, int64_t m = 1 << 30, int64_t n = 1 << 30, int cus = 256) {
-  static int env = -2;
-  if (env == -2) {
-    const char *e = getenv("PMM_GEMM_VARIANT");
-    env = e ? atoi(e) : -1;
-  }
+  // (read per call, so a test can force each variant in turn)
+  const char *ev = getenv("PMM_GEMM_VARIANT");
+  const int env = ev ? atoi(ev) : -1;
   if (env >= 0 && env < 5 && gemm_f32_lds_bytes(env, mode, capg) <= 160 * 1024) return env;
   if (cdiv(m, 256) * cdiv(n, 256) < 4 * (int64_t)cus && gemm_f32_lds_bytes(0, mode, capg) <= 160 * 1024) {
     // 128 x 128 tiles, or for the fused top-k 128 x 64 (variant 4) when its
@@ -377,7 +375,7 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   if (p.capg * 3 / 2 <= 512) p.capg = p.capg * 3 / 2;
   {
     // experiment knob: candidate buffer capacity (>= k + 64, multiple of 8)
-    static const int cap_env = getenv("PMM_CAPG") ? atoi(getenv("PMM_CAPG")) : 0;
+    const int cap_env = getenv("PMM_CAPG") ? atoi(getenv("PMM_CAPG")) : 0;  // (per call)
     if (cap_env > 0 && k + 64 <= 512) p.capg = std::max<int>(((int)k + 64 + 7) / 8 * 8, std::min(cap_env, 512) / 8 * 8);
   }
   const bool bf16 = compute == PMM_COMPUTE_BF16;

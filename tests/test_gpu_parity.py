@@ -617,6 +617,32 @@ def test_merge_schedules_same_lists(pmm, flags, shape, monkeypatch):
     assert_bitexact(got[0][rows], got[1][rows], oi, osc, label=f"merge flags {flags}")
 
 
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
+def test_every_tile_variant_same_lists(pmm, variant, monkeypatch):
+    # each f32 tile variant forced in turn (PMM_GEMM_VARIANT, per call): the
+    # 128-wide ones with the per-lane flag pre-filter, the 256-wide ones with
+    # the two-pass one (flags, wave OR, appends at flagged positions); every
+    # variant returns the default's lists bit for bit, and the oracle's.  A
+    # variant whose LDS carve does not hold the candidate buffers of a k
+    # falls back to the chosen one (k = 300 on 256 x 256).
+    rs = np.random.RandomState(41)
+    m, N, d = 700, 9001, 80
+    q = rs.randn(m, d).astype(np.float32)
+    c = rs.randn(N, d).astype(np.float32)
+    c[17] = 0.0  # a zero-norm corpus row (cosine 0.0, src/metrics.rs:334-337)
+    q[5] = 0.0
+    rows = np.arange(0, m, 53)
+    for metric, mid in (("cosine", oracle.COSINE), ("dot", oracle.DOT), ("euclidean", oracle.EUCLIDEAN)):
+        for k in (1, 37, 100, 300):
+            monkeypatch.delenv("PMM_GEMM_VARIANT", raising=False)
+            want = gpu_topk(q, c, k, metric)
+            monkeypatch.setenv("PMM_GEMM_VARIANT", variant)
+            got = gpu_topk(q, c, k, metric)
+            assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), (variant, metric, k)
+            oi, osc = oracle.topk(q[rows], c, k, mid)
+            assert_bitexact(got[0][rows], got[1][rows], oi, osc, label=f"variant {variant} {metric} k={k}")
+
+
 def test_merge_bytes_counts_the_candidates_left(pmm):
     # the reduction's algorithmic bytes (bench.py "reduction_roofline"):
     # counts + thresholds + output, plus 8 B per candidate the GEMM left --
