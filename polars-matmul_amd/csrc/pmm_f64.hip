@@ -29,71 +29,98 @@ __device__ __forceinline__ double f64_unkey(u64 k, int metric) {
 
 // ---------------------------------------------------------------------------
 // The f64 GEMM tile (store mode and the fused top-k share it, so both paths
-// compute every dot product identically).  64 x 64 tile per 4-wave
-// workgroup, each wave 32 x 32 = 2 x 2 v_mfma_f64_16x16x4_f64 tiles.  K runs
-// in chunks of 16 through a double-buffered LDS image stored k-major
+// compute every dot product identically).  Four waves in 2 x 2; each wave
+// owns W x W v_mfma_f64_16x16x4_f64 tiles (16W x 16W outputs), so the
+// workgroup's tile is 32W x 32W: W = 2 -> 64 x 64, W = 4 -> 128 x 128 (half
+// the operand bytes per flop, four times the MFMAs per LDS fragment pair).
+// K runs in chunks of 16 through a double-buffered LDS image stored k-major
 // (As[k][row]), so at K step s of a chunk lane (i = lane & 15, kq = lane >> 4)
-// reads A[row i][k0 + 4 s + kq] and B[col i][k0 + 4 s + kq] with one
-// ds_read_b64 each: the four MFMAs of a chunk see k0 .. k0 + 15 in natural
-// order.  Rows of 16 + 64 doubles: the kq = 0 and kq = 1 half-waves of a read
-// land on disjoint banks.  Global loads: each thread one 32-byte run (row t/4,
-// k 4(t%4) .. +3) of A and of B per chunk, the next chunk's in flight while
-// this chunk's MFMAs run.  C/D layout: col = lane & 15, row = (lane >> 4) + 4 reg.
+// reads A[row][k0 + 4 s + kq] and B[col][k0 + 4 s + kq] with one ds_read_b64
+// each: the four MFMAs of a chunk see k0 .. k0 + 15 in natural order, whatever
+// W is (so every W returns the same bits).  Rows of 32W + 16 doubles: the
+// kq = 0 and kq = 1 half-waves of a read land on disjoint banks.  Global loads:
+// each thread W / 2 32-byte runs (rows t/4 + 64j, k 4(t%4) .. +3) of A and of
+// B per chunk, the next chunk's in flight while this chunk's MFMAs run.
+// C/D layout: col = lane & 15, row = (lane >> 4) + 4 reg.
 // ---------------------------------------------------------------------------
-constexpr int kF64LdsRow = 80;                              // doubles per LDS row (64 + pad)
-constexpr int kF64LdsBuf = 16 * kF64LdsRow;                 // one operand's chunk
+template <int W>
+struct F64T {
+  static constexpr int R = 32 * W;         // rows (= columns) of a workgroup tile
+  static constexpr int LR = R + 16;        // doubles per LDS k-row
+  static constexpr int BUF = 16 * LR;      // one operand's K chunk
+  static constexpr int LDS = 2 * 2 * BUF;  // two operands, double-buffered
+  static constexpr int NRUN = W / 2;       // staging runs per thread per operand
+  static_assert(W == 2 || W == 4, "64 x 64 or 128 x 128 workgroup tiles");
+};
 
+template <int W>
 __device__ __forceinline__ void f64_tile(const double *__restrict__ q, int64_t ldq, int mrows,
                                          const double *__restrict__ c, int64_t ldc, int ncols, int D,
-                                         f64x4 (&acc)[2][2], double *lds) {
+                                         f64x4 (&acc)[W][W], double *lds) {
+  using T = F64T<W>;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int i = lane & 15, kq = lane >> 4;
-  const int wr = (wid >> 1) * 32, wc = (wid & 1) * 32;
-  // this thread's staging run: row / column lr, k 4 lk .. 4 lk + 3 of a chunk
+  const int wr = (wid >> 1) * 16 * W, wc = (wid & 1) * 16 * W;
+  // this thread's staging runs: rows / columns lr + 64 j, k 4 lk .. 4 lk + 3 of a chunk
   const int lr = tid >> 2, lk = (tid & 3) * 4;
-  const double *ga = q + (int64_t)min(lr, mrows - 1) * ldq + lk;
-  const double *gb = c + (int64_t)min(lr, ncols - 1) * ldc + lk;
-  double *As = lds, *Bs = lds + 2 * kF64LdsBuf;
+  const double *ga[T::NRUN], *gb[T::NRUN];
 #pragma unroll
-  for (int ti = 0; ti < 2; ti++)
+  for (int j = 0; j < T::NRUN; j++) {
+    ga[j] = q + (int64_t)min(lr + 64 * j, mrows - 1) * ldq + lk;
+    gb[j] = c + (int64_t)min(lr + 64 * j, ncols - 1) * ldc + lk;
+  }
+  double *As = lds, *Bs = lds + 2 * T::BUF;
 #pragma unroll
-    for (int tj = 0; tj < 2; tj++) acc[ti][tj] = (f64x4){0.0, 0.0, 0.0, 0.0};
-  f64x2 ra0 = *(const f64x2 *)ga, ra1 = *(const f64x2 *)(ga + 2);
-  f64x2 rb0 = *(const f64x2 *)gb, rb1 = *(const f64x2 *)(gb + 2);
-  auto put = [&](int buf) __attribute__((always_inline)) {
-    double *a = As + buf * kF64LdsBuf + lk * kF64LdsRow + lr;
-    double *b = Bs + buf * kF64LdsBuf + lk * kF64LdsRow + lr;
-    a[0] = ra0[0];
-    a[kF64LdsRow] = ra0[1];
-    a[2 * kF64LdsRow] = ra1[0];
-    a[3 * kF64LdsRow] = ra1[1];
-    b[0] = rb0[0];
-    b[kF64LdsRow] = rb0[1];
-    b[2 * kF64LdsRow] = rb1[0];
-    b[3 * kF64LdsRow] = rb1[1];
+  for (int ti = 0; ti < W; ti++)
+#pragma unroll
+    for (int tj = 0; tj < W; tj++) acc[ti][tj] = (f64x4){0.0, 0.0, 0.0, 0.0};
+  f64x2 ra[T::NRUN][2], rb[T::NRUN][2];
+  auto load = [&](int ko) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < T::NRUN; j++) {
+      ra[j][0] = *(const f64x2 *)(ga[j] + ko);
+      ra[j][1] = *(const f64x2 *)(ga[j] + ko + 2);
+      rb[j][0] = *(const f64x2 *)(gb[j] + ko);
+      rb[j][1] = *(const f64x2 *)(gb[j] + ko + 2);
+    }
   };
+  auto put = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < T::NRUN; j++) {
+      double *a = As + buf * T::BUF + lk * T::LR + lr + 64 * j;
+      double *b = Bs + buf * T::BUF + lk * T::LR + lr + 64 * j;
+      a[0] = ra[j][0][0];
+      a[T::LR] = ra[j][0][1];
+      a[2 * T::LR] = ra[j][1][0];
+      a[3 * T::LR] = ra[j][1][1];
+      b[0] = rb[j][0][0];
+      b[T::LR] = rb[j][0][1];
+      b[2 * T::LR] = rb[j][1][0];
+      b[3 * T::LR] = rb[j][1][1];
+    }
+  };
+  load(0);
   put(0);
   __syncthreads();
   const int nch = D / 16;
   for (int ch = 0; ch < nch; ch++) {
     const int buf = ch & 1;
-    if (ch + 1 < nch) {
-      const int ko = (ch + 1) * 16;
-      ra0 = *(const f64x2 *)(ga + ko);
-      ra1 = *(const f64x2 *)(ga + ko + 2);
-      rb0 = *(const f64x2 *)(gb + ko);
-      rb1 = *(const f64x2 *)(gb + ko + 2);
-    }
-    const double *a = As + buf * kF64LdsBuf + kq * kF64LdsRow + wr + i;
-    const double *b = Bs + buf * kF64LdsBuf + kq * kF64LdsRow + wc + i;
+    if (ch + 1 < nch) load((ch + 1) * 16);
+    const double *a = As + buf * T::BUF + kq * T::LR + wr + i;
+    const double *b = Bs + buf * T::BUF + kq * T::LR + wc + i;
 #pragma unroll
     for (int s = 0; s < 4; s++) {
-      const double a0 = a[4 * s * kF64LdsRow], a1 = a[4 * s * kF64LdsRow + 16];
-      const double b0 = b[4 * s * kF64LdsRow], b1 = b[4 * s * kF64LdsRow + 16];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      double av[W], bv[W];
+#pragma unroll
+      for (int t = 0; t < W; t++) {
+        av[t] = a[4 * s * T::LR + 16 * t];
+        bv[t] = b[4 * s * T::LR + 16 * t];
+      }
+#pragma unroll
+      for (int ti = 0; ti < W; ti++)
+#pragma unroll
+        for (int tj = 0; tj < W; tj++)
+          acc[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti], bv[tj], acc[ti][tj], 0, 0, 0);
     }
     if (ch + 1 < nch) put(buf ^ 1);
     __syncthreads();
@@ -105,10 +132,9 @@ __device__ __forceinline__ void f64_tile(const double *__restrict__ q, int64_t l
 // on logical tile x * ceil(T / 8) + b / 8 (x = b % 8): every XCD walks a
 // contiguous stretch of the logical order, which takes the row blocks in
 // groups of kF64GroupRows (row block fastest inside a group, then the column
-// block): the ~128 workgroups an XCD holds at once share 8 row tiles and ~16
-// column tiles, 3 MB at D = 256, instead of streaming every corpus tile once
-// per row block (a column-block-fastest 2-D grid re-read the corpus from HBM
-// M / 64 times).
+// block): the workgroups an XCD holds at once share 8 row tiles and a few
+// column tiles instead of streaming every corpus tile once per row block (a
+// column-block-fastest 2-D grid re-read the corpus from HBM M / 64 times).
 constexpr int kF64GroupRows = 8;
 __device__ __forceinline__ bool f64_tile_of(int nR, int nC, int &r, int &c) {
   const int64_t T = (int64_t)nR * nC;
@@ -134,19 +160,21 @@ __global__ __launch_bounds__(256) void gemm_f64_store_kernel(const double *__res
                                                              const double *__restrict__ qn,
                                                              const double *__restrict__ cn, int M, int N, int D,
                                                              double *__restrict__ out, int64_t ldo) {
-  __shared__ double lds[2 * 2 * kF64LdsBuf];
+  constexpr int W = 2;
+  using T = F64T<W>;
+  __shared__ double lds[T::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
   int rb, cbk;
-  if (!f64_tile_of((M + 63) / 64, (N + 63) / 64, rb, cbk)) return;
-  const int r0 = rb * 64, c0 = cbk * 64;
-  f64x4 acc[2][2];
-  f64_tile(q + (int64_t)r0 * ldq, ldq, M - r0, c + (int64_t)c0 * ldc, ldc, N - c0, D, acc, lds);
-  const int row0 = r0 + (wid >> 1) * 32, col0 = c0 + (wid & 1) * 32;
+  if (!f64_tile_of((M + T::R - 1) / T::R, (N + T::R - 1) / T::R, rb, cbk)) return;
+  const int r0 = rb * T::R, c0 = cbk * T::R;
+  f64x4 acc[W][W];
+  f64_tile<W>(q + (int64_t)r0 * ldq, ldq, M - r0, c + (int64_t)c0 * ldc, ldc, N - c0, D, acc, lds);
+  const int row0 = r0 + (wid >> 1) * 16 * W, col0 = c0 + (wid & 1) * 16 * W;
 #pragma unroll
-  for (int ti = 0; ti < 2; ti++)
+  for (int ti = 0; ti < W; ti++)
 #pragma unroll
-    for (int tj = 0; tj < 2; tj++)
+    for (int tj = 0; tj < W; tj++)
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int grow = row0 + 16 * ti + kq + 4 * r;
@@ -163,7 +191,8 @@ hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, 
                                  int metric, int store_metric, double *out, int64_t ldo,
                                  hipStream_t s) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  const dim3 grid(f64_grid((M + 63) / 64, (N + 63) / 64)), blk(256);
+  constexpr int R = F64T<2>::R;
+  const dim3 grid(f64_grid((M + R - 1) / R, (N + R - 1) / R)), blk(256);
   if (!store_metric || metric == kMetricDot)
     gemm_f64_store_kernel<kMetricDot, 0><<<grid, blk, 0, s>>>(q, ldq, c, ldc, qn, cn, M, N, D, out, ldo);
   else if (metric == kMetricCosine)
@@ -178,31 +207,32 @@ hipError_t launch_gemm_f64_store(const double *q, int64_t ldq, const double *c, 
 // the exact score (reference order), its key, and an append to the row's
 // buffer when it beats the row's threshold.
 // ---------------------------------------------------------------------------
-template <int METRIC>
-__global__ __launch_bounds__(256) void gemm_f64_topk_kernel(F64TopkArgs a) {
+template <int METRIC, int W>
+__global__ __launch_bounds__(256, W == 4 ? 2 : 1) void gemm_f64_topk_kernel(F64TopkArgs a) {
+  using T = F64T<W>;
   constexpr bool XF = METRIC != kMetricDot;
-  __shared__ double lds[2 * 2 * kF64LdsBuf];
+  __shared__ double lds[T::LDS];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i = lane & 15, kq = lane >> 4;
   int rb, cbk;
-  if (!f64_tile_of((a.M + 63) / 64, (a.ncol + 63) / 64, rb, cbk)) return;
-  const int r0 = rb * 64, lc0w = cbk * 64;  // lc: column within the chunk
-  f64x4 acc[2][2];
-  f64_tile(a.q + (int64_t)r0 * a.ldq, a.ldq, a.M - r0, a.c + (int64_t)(a.col0 + lc0w) * a.ldc, a.ldc,
-           a.ncol - lc0w, a.D, acc, lds);
-  const int row0 = r0 + (wid >> 1) * 32, lc0 = lc0w + (wid & 1) * 32;
+  if (!f64_tile_of((a.M + T::R - 1) / T::R, (a.ncol + T::R - 1) / T::R, rb, cbk)) return;
+  const int r0 = rb * T::R, lc0w = cbk * T::R;  // lc: column within the chunk
+  f64x4 acc[W][W];
+  f64_tile<W>(a.q + (int64_t)r0 * a.ldq, a.ldq, a.M - r0, a.c + (int64_t)(a.col0 + lc0w) * a.ldc, a.ldc,
+              a.ncol - lc0w, a.D, acc, lds);
+  const int row0 = r0 + (wid >> 1) * 16 * W, lc0 = lc0w + (wid & 1) * 16 * W;
   if (a.accept_all) {
     // the first chunk (ncol <= cap): every element at its own column's slot
     // (the counts were set to ncol by the reset; no atomics)
 #pragma unroll
-    for (int ti = 0; ti < 2; ti++)
+    for (int ti = 0; ti < W; ti++)
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const int row = row0 + 16 * ti + kq + 4 * r;
         if (row >= a.M) continue;
         const double qv = XF ? a.qn[row] : 0.0;
 #pragma unroll
-        for (int tj = 0; tj < 2; tj++) {
+        for (int tj = 0; tj < W; tj++) {
           const int lc = lc0 + 16 * tj + i;
           if (lc >= a.ncol) continue;
           const uint32_t gcol = (uint32_t)(a.col0 + lc);
@@ -216,15 +246,32 @@ __global__ __launch_bounds__(256) void gemm_f64_topk_kernel(F64TopkArgs a) {
       }
     return;
   }
-  // Later chunks: every element's key and pass flag first, then one buffer
-  // reservation per (row, wave) -- the 16 lanes of a row group share it --
-  // with all eight in flight, then the appends.  (An atomicAdd per passing
-  // element waited one memory round trip per (row block, register) step:
-  // 0.22 ms for the GEMM at c1 f64 against 0.12 ms in store mode.)
-  u64 key[2][4][2];
-  bool ps[2][4][2];
+  // Later chunks, one 16-row block (ti) at a time: every element's key and
+  // pass flag first, then one buffer reservation per (row, wave) -- the 16
+  // lanes of a row group share it -- with the block's four in flight, then
+  // the appends.  (An atomicAdd per passing element waited one memory round
+  // trip per (row block, register) step: 0.22 ms for the GEMM at c1 f64
+  // against 0.12 ms in store mode.)
+  const u64 grp = 0xFFFFull << (16 * kq);
+  const u64 below = (1ull << lane) - 1ull;
+  // Cosine: the exact score is a division; an element whose dot is below
+  // bm * cn -- bm = ts * qn * (1 -+ 2^-49), ts the row's threshold score --
+  // scores strictly below ts (the three roundings of the bound and the two of
+  // the score are covered 13u > 4u), so it is dropped without the division.
+  // No bound (NaN: never below) for an accept-all row, a zero threshold, a
+  // zero-norm row or column (score 0 whatever the dot), or a NaN.
+  const double kNaN = __longlong_as_double(0x7FF8000000000000ll);
+  double cnf[W];
 #pragma unroll
-  for (int ti = 0; ti < 2; ti++)
+  for (int tj = 0; tj < W; tj++) {
+    const int lc = lc0 + 16 * tj + i;
+    const double cvv = (METRIC == kMetricCosine && lc < a.ncol) ? a.cn[a.col0 + lc] : 0.0;
+    cnf[tj] = cvv > 1e-10 ? cvv : kNaN;
+  }
+#pragma unroll
+  for (int ti = 0; ti < W; ti++) {
+    u64 key[4][W];
+    bool ps[4][W];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int row = row0 + 16 * ti + kq + 4 * r;
@@ -232,59 +279,79 @@ __global__ __launch_bounds__(256) void gemm_f64_topk_kernel(F64TopkArgs a) {
       const u64 tk = rv ? a.tkey[row] : ~0ull;
       const uint32_t tx = rv ? a.tidx[row] : 0u;
       const double qv = (XF && rv) ? a.qn[row] : 0.0;
+      double bm = kNaN;
+      if (METRIC == kMetricCosine) {
+        const double ts = dekey64(tk);
+        if (qv > 1e-10 && ts != 0.0)
+          bm = __dmul_rn(__dmul_rn(ts, qv), ts > 0.0 ? 1.0 - 0x1p-49 : 1.0 + 0x1p-49);
+      }
 #pragma unroll
-      for (int tj = 0; tj < 2; tj++) {
+      for (int tj = 0; tj < W; tj++) {
         const int lc = lc0 + 16 * tj + i;
         const bool cv = rv && lc < a.ncol;
         const uint32_t gcol = (uint32_t)(a.col0 + lc);
         const double v = acc[ti][tj][r];
+        key[r][tj] = 0ull;
+        ps[r][tj] = false;
+        if (METRIC == kMetricCosine && v < __dmul_rn(bm, cnf[tj])) continue;
         const double sc = XF ? exact_score_f64<METRIC>(v, qv, cv ? a.cn[gcol] : 0.0) : v;
-        key[ti][r][tj] = f64_key(sc, METRIC);
-        ps[ti][r][tj] = cv && (key[ti][r][tj] > tk || (key[ti][r][tj] == tk && gcol < tx));
+        key[r][tj] = f64_key(sc, METRIC);
+        ps[r][tj] = cv && (key[r][tj] > tk || (key[r][tj] == tk && gcol < tx));
       }
     }
-  const u64 grp = 0xFFFFull << (16 * kq);
-  const u64 below = (1ull << lane) - 1ull;
-  unsigned base[2][4];
-#pragma unroll
-  for (int ti = 0; ti < 2; ti++)
+    unsigned base[4];
 #pragma unroll
     for (int r = 0; r < 4; r++) {
-      const u64 m0 = __ballot(ps[ti][r][0]) & grp, m1 = __ballot(ps[ti][r][1]) & grp;
-      const unsigned n = (unsigned)(__popcll(m0) + __popcll(m1));
+      unsigned n = 0u;
+#pragma unroll
+      for (int tj = 0; tj < W; tj++) n += (unsigned)__popcll(__ballot(ps[r][tj]) & grp);
       unsigned b0 = 0u;
       if (i == 0 && n != 0u) b0 = atomicAdd(a.cnt + row0 + 16 * ti + kq + 4 * r, n);
-      base[ti][r] = b0;
+      base[r] = b0;
     }
-#pragma unroll
-  for (int ti = 0; ti < 2; ti++)
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int row = row0 + 16 * ti + kq + 4 * r;
-      const unsigned b0 = (unsigned)__shfl((int)base[ti][r], lane & 48, 64);
-      const u64 m0 = __ballot(ps[ti][r][0]) & grp, m1 = __ballot(ps[ti][r][1]) & grp;
+      unsigned pos = (unsigned)__shfl((int)base[r], lane & 48, 64);
 #pragma unroll
-      for (int tj = 0; tj < 2; tj++) {
-        if (!ps[ti][r][tj]) continue;
-        const unsigned pos = b0 + (tj ? (unsigned)(__popcll(m0) + __popcll(m1 & below)) : (unsigned)__popcll(m0 & below));
-        if (pos < (unsigned)a.cap) {
+      for (int tj = 0; tj < W; tj++) {
+        const u64 m = __ballot(ps[r][tj]) & grp;
+        if (ps[r][tj] && pos + (unsigned)__popcll(m & below) < (unsigned)a.cap) {
           Ent e;
-          e.key = key[ti][r][tj];
+          e.key = key[r][tj];
           e.idx = (uint32_t)(a.col0 + lc0 + 16 * tj + i);
           e.pad = 0u;
-          a.cand[(int64_t)row * a.cap + pos] = e;
+          a.cand[(int64_t)row * a.cap + pos + __popcll(m & below)] = e;
         }
+        pos += (unsigned)__popcll(m);
       }
     }
+  }
+}
+
+// 64 x 64 tiles: 128 x 128 ones (W = 4, two waves per SIMD, half the
+// operand bytes per flop) measured slower at 4096 x 1M x 256: the fused GEMM
+// 43.0 vs 39.7-39.8 ms per step, alternated on one box
+// (profiles/r5_f64/ab.txt) -- the f64 kernel is bound by its issue, not its
+// operand stream.  PMM_F64_TILE=128 (per call) keeps them for tests / A/B.
+
+template <int W>
+static hipError_t launch_gemm_f64_topk_w(const F64TopkArgs &a, hipStream_t s) {
+  constexpr int R = F64T<W>::R;
+  const dim3 grid(f64_grid((a.M + R - 1) / R, (a.ncol + R - 1) / R)), blk(256);
+  if (a.metric == kMetricCosine) gemm_f64_topk_kernel<kMetricCosine, W><<<grid, blk, 0, s>>>(a);
+  else if (a.metric == kMetricEuclidean) gemm_f64_topk_kernel<kMetricEuclidean, W><<<grid, blk, 0, s>>>(a);
+  else gemm_f64_topk_kernel<kMetricDot, W><<<grid, blk, 0, s>>>(a);
+  return hipGetLastError();
 }
 
 hipError_t launch_gemm_f64_topk(const F64TopkArgs &a, hipStream_t s) {
   if (a.M <= 0 || a.ncol <= 0) return hipSuccess;
-  const dim3 grid(f64_grid((a.M + 63) / 64, (a.ncol + 63) / 64)), blk(256);
-  if (a.metric == kMetricCosine) gemm_f64_topk_kernel<kMetricCosine><<<grid, blk, 0, s>>>(a);
-  else if (a.metric == kMetricEuclidean) gemm_f64_topk_kernel<kMetricEuclidean><<<grid, blk, 0, s>>>(a);
-  else gemm_f64_topk_kernel<kMetricDot><<<grid, blk, 0, s>>>(a);
-  return hipGetLastError();
+  // (PMM_F64_TILE=64 / 128 forces one size, per call: tests and A/B runs)
+  const char *e = getenv("PMM_F64_TILE");
+  const int force = e ? atoi(e) : 0;
+  if (force == 128) return launch_gemm_f64_topk_w<4>(a, s);
+  return launch_gemm_f64_topk_w<2>(a, s);
 }
 
 // ---------------------------------------------------------------------------

@@ -181,13 +181,18 @@ def test_f64_fixture_vs_oracle(pmm, metric):
 @pytest.mark.parametrize("m,n,d,k", [(48, 1000, 256, 50), (33, 30011, 37, 10), (7, 9000, 100, 1),
                                      (64, 20000, 64, 100), (5, 3000, 16, 1000), (130, 700, 200, 700)])
 @pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
-def test_f64_fused_vs_oracle_and_materialised(pmm, m, n, d, k, metric, monkeypatch):
+@pytest.mark.parametrize("tile", ["64", "128"])
+def test_f64_fused_vs_oracle_and_materialised(pmm, m, n, d, k, metric, tile, monkeypatch):
+    # tile: the fused kernel's workgroup tile (PMM_F64_TILE: 64 x 64 by
+    # default, 128 x 128 forced) -- K order is the same, so the same bits
+    monkeypatch.setenv("PMM_F64_TILE", tile)
     rs = np.random.RandomState(m * 7 + n + d + k)
     q = rs.randn(m, d)
     c = rs.randn(n, d)
     c[n - 30:] = c[:30]  # exact ties across chunk boundaries
     c[n // 2] = 0.0      # a zero-norm corpus row
     q[0] = c[5]          # a query equal to a corpus row
+    q[-1] = 0.0 if m > 1 else q[-1]  # a zero-norm query row (every cosine score 0)
     monkeypatch.setenv("PMM_F64_FUSED", "1")  # (by size these shapes take the materialised path)
     idx, sc = gpu_topk(q, c, k, metric)
     assert sc.dtype == np.float64 and idx.shape == (m, min(k, n))
@@ -232,8 +237,11 @@ def test_f64_fused_overflow_falls_back(pmm, monkeypatch):
     assert np.array_equal(idx, oi) and np.array_equal(sc, osc)
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("fused", ["1", "1-128", "0"])
 def test_f64_nan_rows_and_k_equals_n(pmm, fused, monkeypatch):
+    if fused == "1-128":
+        fused = "1"
+        monkeypatch.setenv("PMM_F64_TILE", "128")
     monkeypatch.setenv("PMM_F64_FUSED", fused)
     rs = np.random.RandomState(5)
     q, c = rs.randn(9, 24), rs.randn(1500, 24)
