@@ -1216,7 +1216,7 @@ def main():
     ap.add_argument("--inproc", type=int, default=1,
                     help="N > 1: after the RCCL ranks, also measure the in-process transport (one child "
                          "process driving all N GPUs through pmm_set_devices) under extra.inproc")
-    ap.add_argument("--inproc-timeout", type=int, default=900, help=argparse.SUPPRESS)
+    ap.add_argument("--inproc-timeout", type=int, default=300, help=argparse.SUPPRESS)
     ap.add_argument("--inproc-child", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.metric and args.metric != CONFIGS[args.config][4]:
