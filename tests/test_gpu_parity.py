@@ -223,6 +223,35 @@ def test_f64_fused_scores_bitwise_vs_oracle(pmm, fused, monkeypatch):
         assert np.array_equal(sc.view(np.uint64), osc.view(np.uint64)), metric
 
 
+@pytest.mark.parametrize("k", [5, 40, 120, 700, 1500])
+def test_f64_cosine_division_skip_at_threshold_edges(pmm, k, monkeypatch):
+    # the fused f64 kernel drops cosine elements whose dot is below the row's
+    # threshold bound without dividing (pmm_f64.hip): thresholds here land on
+    # positive scores, on exact zeros (orthogonal rows, zero-norm rows: no
+    # bound), on negative scores, and on runs of exact ties -- the lists must
+    # equal the oracle's and the materialised path's bit for bit
+    monkeypatch.setenv("PMM_F64_FUSED", "1")
+    rs = np.random.RandomState(k)
+    n, d = 3000, 8
+    q = np.zeros((6, d))
+    q[:, 0] = 1.0
+    q[3] = rs.randn(d)
+    q[5] = 0.0                                  # a zero-norm query row
+    c = rs.randn(n, d)
+    c[:100, 0] = np.abs(c[:100, 0]) + 0.5       # 100 positive scores for the e1 queries
+    c[100:1100, 0] = 0.0                        # 1000 exact zeros (orthogonal)
+    c[1100:1600] = c[1100]                      # 500 exact ties
+    c[1600:1700] = 0.0                          # zero-norm corpus rows (score 0 by rule)
+    c[1700:, 0] = -np.abs(c[1700:, 0]) - 0.1    # negative scores
+    idx, sc = gpu_topk(q, c, k, "cosine")
+    oi, osc = oracle.topk(q, c, k, METRICS["cosine"])
+    assert np.array_equal(idx, oi), f"k={k}"
+    assert np.array_equal(sc.view(np.uint64), osc.view(np.uint64)), f"k={k}"
+    monkeypatch.setenv("PMM_F64_FUSED", "0")
+    mi, ms = gpu_topk(q, c, k, "cosine")
+    assert np.array_equal(mi, idx) and np.array_equal(ms.view(np.uint64), sc.view(np.uint64))
+
+
 def test_f64_fused_overflow_falls_back(pmm, monkeypatch):
     # adversarial order: every corpus row beats every earlier one, so each
     # chunk's survivors overflow the buffers; the call must still be exact
