@@ -94,3 +94,46 @@ def test_detector_flags_a_spill_in_an_mfma_block():
         "\ts_endpgm",
     ])
     assert mfma_blocks_with_spills(asm) == [("_Zkern", ".LBB0_1")]
+
+
+def _makefile_var(name):
+    import os
+    mk = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "polars-matmul_amd", "Makefile")
+    for line in open(mk):
+        m = re.match(rf"^{name}\s*:?=\s*(.*)$", line.strip())
+        if m:
+            return m.group(1).split()
+    raise KeyError(name)
+
+
+@pytest.mark.skipif(not have_hipcc(), reason="hipcc not available")
+def test_f64_mfmas_keep_their_accumulators_in_vgprs():
+    # pmm_f64.hip is built with the MFMAs in their VGPR form (Makefile
+    # F64_FLAGS): with the compiler's AGPR choice every 16-wide K chunk copied
+    # the accumulators VGPR -> AGPR and back (64 v_accvgpr moves per 16 MFMAs,
+    # 42.1 vs 39.8 ms at 4096 x 1M x 256).  Every f64 MFMA kernel of the
+    # product build must be free of accumulator moves.
+    import os
+    import subprocess
+    import tempfile
+
+    from isa_util import CSRC, FLAGS, HIPCC
+
+    with tempfile.TemporaryDirectory() as tmp:
+        out = os.path.join(tmp, "f64.s")
+        subprocess.run([HIPCC, *FLAGS, *_makefile_var("F64_FLAGS"), "-I", CSRC, "-o", out,
+                        os.path.join(CSRC, "pmm_f64.hip")], check=True, capture_output=True, timeout=600)
+        asm = open(out).read()
+    funcs, func = {}, None
+    for line in asm.splitlines():
+        if re.match(r"^_Z\S+:", line):
+            func = line.split(":")[0]
+            funcs[func] = [0, 0]
+        elif func:
+            s = line.strip()
+            funcs[func][0] += s.startswith("v_mfma_f64")
+            funcs[func][1] += s.startswith("v_accvgpr")
+    mfma = {f: c for f, c in funcs.items() if c[0]}
+    assert len(mfma) >= 6, sorted(mfma)  # store (3 metrics) + top-k (3 metrics x 2 tiles)
+    bad = {f: c[1] for f, c in mfma.items() if c[1]}
+    assert not bad, f"accumulator moves in f64 MFMA kernels: {bad}"
