@@ -599,11 +599,40 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
   a.wq = (unsigned long long *)(w + p.off_wq);
   a.cnt = (unsigned *)(w + p.off_cnt);
   a.gthr = (unsigned long long *)(w + p.off_gthr);
+#ifdef PMM_LAB
+  // per-phase cycle counters of the f32 kernel (make lab LAB=-DPMM_F32_STATS,
+  // PMM_STATS=1): summed over waves, printed per call
+  static const bool f32_stats = getenv("PMM_STATS") != nullptr;
+  static unsigned long long *f32_stats_buf = nullptr;
+  if (f32_stats) {
+    if (!f32_stats_buf) {
+      hipError_t e = hipMalloc(&f32_stats_buf, 128);
+      if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipMemsetAsync(f32_stats_buf, 0, 128, s);
+    if (e != hipSuccess) return e;
+    a.stats = f32_stats_buf;
+  }
+#endif
   {
     Timed t(gemm_label, s);
     hipError_t e = launch_gemm_f32(a, p.variant, 0, p.grid, s);
     if (e != hipSuccess) return e;
   }
+#ifdef PMM_LAB
+  if (f32_stats) {
+    unsigned long long h[16];
+    hipError_t e = hipMemcpyAsync(h, f32_stats_buf, 128, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    fprintf(stderr,
+            "[pmm stats] gemm_f32 variant %d: units %d, S %d, tps %d, grid %d; wave cycles (sum): total %.4g, "
+            "unit setup %.4g, K loops %.4g (barriers %.4g), epilogues %.4g; wave-tiles %llu\n",
+            p.variant, p.units, p.S, p.tps, p.grid, (double)h[0], (double)h[4], (double)h[2], (double)h[1],
+            (double)h[3], h[5]);
+    a.stats = nullptr;
+  }
+#endif
   MergeArgs ma{};
   ma.cand = a.cand;
   ma.cnt = a.cnt;

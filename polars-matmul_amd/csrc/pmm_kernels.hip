@@ -195,6 +195,17 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   float *qex_w = qex_l + wid * 32;  // per-row constants live in LDS, not in VGPRs
   float *lo_w = lo_l + wid * 32;    // across the K loop (keeps 256x256 spill-free)
   constexpr bool XFORM = (METRIC != kMetricDot);
+  // (lab build with -DPMM_F32_STATS and PMM_STATS=1: per-wave phase cycles,
+  // summed over waves -- s_memtime reads, one vector atomic per counter at
+  // the end)
+#ifdef PMM_F32_STATS
+  const bool timing = a.stats != nullptr;
+#else
+  constexpr bool timing = false;
+#endif
+  auto stamp = [&]() __attribute__((always_inline)) { return timing ? __builtin_amdgcn_s_memtime() : 0ull; };
+  const uint64_t t_start = stamp();
+  uint64_t cy_bar = 0, cy_loop = 0, cy_epi = 0, cy_unit = 0, n_tiles = 0;
 
   // Loop-invariant per-lane byte offsets of this wave's LDS-DMA pieces.
   // Gathered image (4-byte pieces of 256 LDS bytes = 2 rows): LDS dword p of
@@ -242,6 +253,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
 
   int buf = 0;
   for (;;) {
+    const uint64_t tu0 = stamp();
     if (tid == 0) *unit_l = (int)atomicAdd(a.counter, 1u);
     __syncthreads();
     const int unit = *unit_l;
@@ -376,7 +388,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         }
     }
     stage(buf, rb, 0, t0, 0, TP);
+    if (timing) cy_unit += stamp() - tu0;
     for (int tile = t0; tile < t1; tile++) {
+      const uint64_t tl0 = stamp();
       const bool last_tile = (tile + 1) >= t1;
       const __amdgpu_buffer_rsrc_t rbn = last_tile ? rb : rsrc_b(tile + 1);
       f32x16 acc[NB];
@@ -392,7 +406,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       // one K step; DEF: defer its last substep, PREV: run the previous
       // step's deferred substep first (compile-time, so no per-substep branch)
       auto kstep = [&](int ks, auto DEF, auto PREV) __attribute__((always_inline)) {
+        const uint64_t tb0 = stamp();
         __syncthreads();  // stage `buf` landed (vmcnt(0) + barrier); buf^1 free
+        if (timing) cy_bar += stamp() - tb0;
         const char *st = smem + buf * G::STAGE;
         // KORDER 0: lane half h covers k = 16h..16h+15 (substep j of group
         // qd pairs k = 4qd+j with 16+4qd+j).  Otherwise half h reads chunk
@@ -483,6 +499,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         kstep(KS - 1, No{}, Yes{});
       }
       rb = rbn;
+      const uint64_t te0 = stamp();
+      if (timing) {
+        cy_loop += te0 - tl0;
+        n_tiles++;
+      }
 
       const int col0 = tile * G::BN;
       if (PMM_ABL(a.ablate) == 1 || PMM_ABL(a.ablate) == 4) {
@@ -690,6 +711,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           }
         }
       }
+      if (timing) cy_epi += stamp() - te0;
     }
 
     if (MODE == 0) {
@@ -698,6 +720,14 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         if (grow < a.M) a.cnt[(int64_t)grow * a.S + s] = cnt_w[lane];
       }
     }
+  }
+  if (timing && lane == 0) {
+    atomicAdd(a.stats + 0, (u64)(stamp() - t_start));
+    atomicAdd(a.stats + 1, (u64)cy_bar);
+    atomicAdd(a.stats + 2, (u64)cy_loop);
+    atomicAdd(a.stats + 3, (u64)cy_epi);
+    atomicAdd(a.stats + 4, (u64)cy_unit);
+    atomicAdd(a.stats + 5, (u64)n_tiles);
   }
 }
 
