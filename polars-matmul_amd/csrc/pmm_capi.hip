@@ -627,9 +627,10 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
     if (e != hipSuccess) return e;
     fprintf(stderr,
             "[pmm stats] gemm_f32 variant %d: units %d, S %d, tps %d, grid %d; wave cycles (sum): total %.4g, "
-            "unit setup %.4g, K loops %.4g (barriers %.4g), epilogues %.4g; wave-tiles %llu\n",
+            "unit setup %.4g, K loops %.4g (barriers %.4g), epilogues %.4g (pre-filter + queueing %.4g, "
+            "compactions %.4g; CNL flags + prefix sum %.4g); wave-tiles %llu, queued survivors %llu\n",
             p.variant, p.units, p.S, p.tps, p.grid, (double)h[0], (double)h[4], (double)h[2], (double)h[1],
-            (double)h[3], h[5]);
+            (double)h[3], (double)h[6], (double)h[7], (double)h[9], h[5], h[8]);
     a.stats = nullptr;
   }
 #endif

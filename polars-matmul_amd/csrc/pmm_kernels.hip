@@ -205,7 +205,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
 #endif
   auto stamp = [&]() __attribute__((always_inline)) { return timing ? __builtin_amdgcn_s_memtime() : 0ull; };
   const uint64_t t_start = stamp();
-  uint64_t cy_bar = 0, cy_loop = 0, cy_epi = 0, cy_unit = 0, n_tiles = 0;
+  uint64_t cy_bar = 0, cy_loop = 0, cy_epi = 0, cy_unit = 0, n_tiles = 0, cy_pf = 0, cy_comp = 0, n_surv = 0, cy_flags = 0;
 
   // Loop-invariant per-lane byte offsets of this wave's LDS-DMA pieces.
   // Gathered image (4-byte pieces of 256 LDS bytes = 2 rows): LDS dword p of
@@ -589,6 +589,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             excl += lanes_below(m) << j;
             tot += __popcll(m) << j;
           }
+          if (timing) cy_flags += stamp() - te0;
           if (bits && PMM_ABL(a.ablate) != 2) {
             int qi = qlen + excl;
 #pragma unroll
@@ -669,6 +670,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           }
         }
 #endif
+        if (timing) {
+          cy_pf += stamp() - te0;
+          n_surv += (uint64_t)qlen;
+        }
         if (PMM_ABL(a.ablate) == 2) qlen = 0;  // ablation: pre-filter only
         if (qlen) {
           // queue entries past the LDS part: their stores reached L2
@@ -699,6 +704,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
             u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 64));
             if (need) {
+              const uint64_t tc0 = stamp();
               asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
               while (need) {
                 const int r = __builtin_ctzll(need);
@@ -707,6 +713,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
               }
               if (lane < 32) lo_w[lane] = prefilter_bound<METRIC>(thr_w[lane], qex_w[lane]);
               wave_sync();
+              if (timing) cy_comp += stamp() - tc0;
             }
           }
         }
@@ -728,6 +735,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     atomicAdd(a.stats + 3, (u64)cy_epi);
     atomicAdd(a.stats + 4, (u64)cy_unit);
     atomicAdd(a.stats + 5, (u64)n_tiles);
+    atomicAdd(a.stats + 6, (u64)cy_pf);
+    atomicAdd(a.stats + 7, (u64)cy_comp);
+    atomicAdd(a.stats + 8, (u64)n_surv);
+    atomicAdd(a.stats + 9, (u64)cy_flags);
   }
 }
 
