@@ -364,6 +364,9 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
 #ifndef PMM_F32_PF2
 #define PMM_F32_PF2 1
 #endif
+#ifndef PMM_F32_FLAT_QUEUE
+#define PMM_F32_FLAT_QUEUE 1
+#endif
 #ifndef PMM_F32_FRAG_PREFETCH
 #define PMM_F32_FRAG_PREFETCH 1  // (A/B: 0 off, 1 the 128 x 128 variant only, 2 every variant)
 #endif
@@ -599,8 +602,15 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
                 if ((bits >> (16 * c + e)) & 1ull) {
                   const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
                   const u64 item = (u64)__float_as_uint(acc[c][e]) | ((u64)hi << 32);
+#if PMM_F32_FLAT_QUEUE
+                  // one generic (flat) store, LDS or global by address: no
+                  // second divergent branch per position
+                  u64 *dst = qi < a.qcap ? lq + qi : gq + qi;
+                  *dst = item;
+#else
                   if (qi < a.qcap) lq[qi] = item;
                   else gq[qi] = item;
+#endif
                   qi++;
                 }
           }
