@@ -331,7 +331,7 @@ __global__ __launch_bounds__(NW * 64, 1) void gemm_bf16_kernel(GemmF32Args a) {
         // compact every row whose buffer could overflow on the next 64 appends
         wave_sync();
         const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
-        u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 64));
+        u64 need = __ballot(lane < 32 && cval > (unsigned)a.ctrig);
         if (need) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           st_c += (uint32_t)__popcll(need);

@@ -572,9 +572,19 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
       const uint32_t lq_lds = (uint32_t)(size_t)(LDS_AS char *)(smem + C::OFF_QUEUE) + rw * QCAP * 8;
       const u64 *lq = (const u64 *)(smem + C::OFF_QUEUE) + rw * QCAP;
       int qlen = 0;  // wave-uniform
+      // A split unit (phase B) shares its rows with the other splits' units:
+      // their compactions raise the rows' shared thresholds (gthr) while this
+      // unit runs, so every drain re-reads them (relaxed, agent scope: any
+      // value read is some unit's k-th best of its own segment, a lower bound
+      // of the row's final k-th) and prunes with the larger bound.  The load
+      // is issued at the drain's start and consumed at its end.
+      const bool split_unit = u.first && u.last && a.S > 1;
       auto drain = [&]() __attribute__((always_inline)) {
         const uint64_t td0 = stamp();
         if (timing) nq += (uint64_t)qlen;
+        u64 gt = 0ull;
+        if (split_unit && lane < 32 && wrow0 + lane < a.M)
+          gt = __hip_atomic_load(a.gthr + wrow0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         for (int base = 0; base < qlen; base += 64) {
           const int i = base + lane;
           if (i < qlen) {
@@ -595,7 +605,7 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
           // overflow on the next round
           wave_sync();
           const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
-          u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 64));
+          u64 need = __ballot(lane < 32 && cval > (unsigned)a.ctrig);
           if (need) {
             const uint64_t tc0 = stamp();
             if (timing) ncomp += (uint64_t)__popcll(need);
@@ -611,6 +621,14 @@ __global__ __launch_bounds__(ws::NTH, 1) void gemm_bf16_ws_kernel(GemmF32Args a)
             load_lo();
             if (timing) cy4 += stamp() - tc0;
           }
+        }
+        if (split_unit) {
+          if (lane < 32 && gt > thr_w[lane]) {
+            thr_w[lane] = gt;
+            lo_w[lane] = prefilter_bound<METRIC>(gt, qex_w[lane]);
+          }
+          wave_sync();
+          load_lo();
         }
         qlen = 0;
         if (timing) cy6 += stamp() - td0;

@@ -235,6 +235,7 @@ struct Timed {
 struct Plan {
   int variant = 0;
   int QB = 0, T = 0, tps = 0, S = 0, units = 0, grid = 0, capg = 0, P = 0, qb_full = 0;
+  int ctrig = 0;  // compaction trigger (GemmF32Args::ctrig)
   size_t off_counter = 0, off_gthr = 0, off_cnt = 0, off_cand = 0, off_qn = 0, off_cn = 0;
   size_t off_wq = 0;
   // fire-and-forget bf16 kernel (variant -6): guess sample size and rank,
@@ -427,6 +428,14 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
     p.ffcap = (int)(((int64_t)(1.5 * 64.0 * e_rs) + 256 + 63) / 64 * 64);
     if (const char *ce = getenv("PMM_FF_CAP")) p.ffcap = std::max(64, atoi(ce));  // (tests: force overflows)
   }
+  // Compaction trigger: a row's buffer is compacted (its k-th selected, the
+  // row threshold raised to it) once it holds more than ctrig entries.  A
+  // drain round adds at most 64 per row, so ctrig <= capg - 64.
+  p.ctrig = p.capg - 64;
+  if (const char *te = getenv("PMM_CTRIG")) {  // (experiment knob, per call)
+    const int t = atoi(te);
+    if (t > 0) p.ctrig = std::max<int>((int)k + 8, std::min(t, p.capg - 64));
+  }
   // merge_kernel's per-row LDS capacity: at least 512, so a row's candidate
   // lists rarely need a compaction before the final one (c1: ~400 survivors
   // of the seed threshold per row; P = 128 compacted ~6 times, 23 us)
@@ -581,6 +590,7 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
   a.D = (int)f.dp;
   a.k = (int)f.k;
   a.capg = p.capg;
+  a.ctrig = p.ctrig;
   a.metric = f.metric;
   a.QB = p.QB;
   a.S = p.S;
@@ -862,6 +872,7 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
   a.D = (int)dp;
   a.k = (int)k;
   a.capg = p.capg;
+  a.ctrig = p.ctrig;
   a.metric = metric;
   a.QB = p.QB;
   a.S = p.S;

@@ -41,6 +41,8 @@ struct GemmF32Args {
   int64_t ldq, ldc;
   int M, N, D;          // D % 32 == 0
   int k, capg;          // top-k and candidate-buffer capacity (power of two)
+  int ctrig;            // compaction trigger: a row's buffer is compacted to its best k
+                        // once it holds more than ctrig entries (k < ctrig <= capg - 64)
   int metric;
   int QB, S, tps, ntiles, units;  // work decomposition (see plan_units)
   unsigned *counter;              // work-queue head, zeroed per call

@@ -712,7 +712,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             // compact every row whose buffer could overflow on the next 64 appends
             wave_sync();
             const unsigned cval = (lane < 32) ? cnt_w[lane] : 0u;
-            u64 need = __ballot(lane < 32 && cval > (unsigned)(a.capg - 64));
+            u64 need = __ballot(lane < 32 && cval > (unsigned)a.ctrig);
             if (need) {
               const uint64_t tc0 = stamp();
               asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

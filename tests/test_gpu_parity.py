@@ -1061,6 +1061,47 @@ def test_bf16_whole_block_runs(pmm, metric, whole, monkeypatch):
     assert match / (m * k) > 0.97
 
 
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_compaction_trigger_leaves_lists_unchanged(pmm, metric, monkeypatch):
+    # PMM_CTRIG (the count above which a row's candidate buffer is compacted
+    # and its threshold raised) changes how many survivors are queued, never
+    # the result: bf16 (whole blocks + split units, the split units re-reading
+    # the shared thresholds at every drain) and f32, bit for bit against the
+    # default trigger.
+    import torch
+
+    n = _native()
+    monkeypatch.setenv("PMM_CUS", "16")
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    m, N, d, k = 4480, 60000, 256, 100
+    q = torch.randn((m, d), generator=g, device=dev).to(torch.bfloat16)
+    c = torch.randn((N, d), generator=g, device=dev).to(torch.bfloat16)
+
+    def run_bf16():
+        oi = torch.empty((m, k), dtype=torch.int32, device=dev)
+        osc = torch.empty((m, k), dtype=torch.float32, device=dev)
+        n.topk_bf16_device(q.data_ptr(), d, m, c.data_ptr(), d, N, d, k, METRICS[metric],
+                           oi.data_ptr(), osc.data_ptr(), stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        return oi.cpu().numpy(), osc.cpu().numpy()
+
+    qf = q[:512].float().cpu().numpy()
+    cf = c[:20000].float().cpu().numpy()
+    monkeypatch.delenv("PMM_CTRIG", raising=False)
+    ref_b = run_bf16()
+    ref_f = gpu_topk(qf, cf, k, metric)
+    for t in ("108", "160", "300"):
+        monkeypatch.setenv("PMM_CTRIG", t)
+        got_b = run_bf16()
+        assert np.array_equal(got_b[0], ref_b[0]), (metric, t)
+        assert np.array_equal(got_b[1].view(np.uint32), ref_b[1].view(np.uint32)), (metric, t)
+        got_f = gpu_topk(qf, cf, k, metric)
+        assert np.array_equal(got_f[0], ref_f[0]), (metric, t)
+        assert np.array_equal(np.asarray(got_f[1], np.float64), np.asarray(ref_f[1], np.float64)), (metric, t)
+
+
 def test_bf16_limits_raise(pmm):
     n = _native()
     q = np.zeros((2, 800), np.float32)
