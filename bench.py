@@ -263,6 +263,37 @@ def numpy_comparator(q, c, k, reps=1, warm=0):
     return q.shape[0] / dt, dt
 
 
+def link_ceilings(out_bytes, in_bytes, reps=5):
+    """The box's host <-> device copy rates: one
+    hipMemcpyAsync (torch copy_) of out_bytes device -> page-locked host, and
+    of in_bytes host -> device from page-locked and from pageable memory,
+    median of `reps` after one warm-up each."""
+    import torch
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    d_out = torch.empty(out_bytes // 4, dtype=torch.float32, device=dev)
+    h_out = torch.empty(out_bytes // 4, dtype=torch.float32, pin_memory=True)
+    d_in = torch.empty(in_bytes // 4, dtype=torch.float32, device=dev)
+    h_in_pinned = torch.ones(in_bytes // 4, dtype=torch.float32, pin_memory=True)
+    h_in_pageable = torch.ones(in_bytes // 4, dtype=torch.float32)
+
+    def rate(dst, src, nbytes):
+        dst.copy_(src, non_blocking=True)
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return round(nbytes / float(np.median(ts)) / 1e9, 2)
+
+    out = {"d2h_pinned_gbs": rate(h_out, d_out, out_bytes), "h2d_pinned_gbs": rate(d_in, h_in_pinned, in_bytes),
+           "h2d_pageable_gbs": rate(d_in, h_in_pageable, in_bytes), "out_bytes": out_bytes, "in_bytes": in_bytes}
+    del d_out, h_out, d_in, h_in_pinned, h_in_pageable
+    return out
+
+
 def matmul_line(args, reps=20, warm=3):
     """SURVEY 8f row 1, `.pmm.matmul` (matmul.rs:295-417): the f32 GEMM in store
     mode through the host C ABI (pmm_matmul_f32: host Q, C in; the M x N f32
@@ -305,6 +336,9 @@ def matmul_line(args, reps=20, warm=3):
     dt = float(np.median(ts))
     rdt = float(np.median(rts))
     flops = 2.0 * M * N * D
+    link = link_ceilings(out_bytes=M * N * 4, in_bytes=(M + N) * D * 4)
+    link_floor_ms = (M + N) * D * 4 / (link["h2d_pageable_gbs"] * 1e9) * 1000.0 + \
+        M * N * 4 / (link["d2h_pinned_gbs"] * 1e9) * 1000.0
     line = {
         "metric": f"matmul calls/s ({M}x{N}x{D} f32, host buffers in and out)", "value": round(1.0 / dt, 2),
         "unit": "calls/s", "ms_per_call": round(dt * 1000.0, 3),
@@ -312,6 +346,11 @@ def matmul_line(args, reps=20, warm=3):
         "kernel_tflops": round(flops / (kms / kn / 1000.0) / 1e12, 2) if kn else None,
         "ms_per_call_reused_out": round(rdt * 1000.0, 3),
         "out_gbs": round(M * N * 4 / dt / 1e9, 2), "max_rel_err_vs_f64": err,
+        "d2h_ceiling_gbs": link["d2h_pinned_gbs"], "out_frac_of_d2h": round(M * N * 4 / dt / 1e9 / link["d2h_pinned_gbs"], 3),
+        "link": link,
+        # the call's bytes over the link at the measured rates (inputs from
+        # pageable NumPy memory, the result into page-locked blocks), serialised
+        "link_floor_ms": round(link_floor_ms, 3), "link_frac": round(link_floor_ms / (dt * 1000.0), 3),
         "note": "result bytes M*N*4 = 40 MB per call, copied into a pooled page-locked block: the "
                 "PCIe copy, not the GEMM, bounds the call",
     }
@@ -331,6 +370,82 @@ def matmul_line(args, reps=20, warm=3):
             "host_nproc": os.cpu_count(), "available_parallelism": available_parallelism(), "kind": "port",
             "sample": f"the full product, NumPy f32 BLAS q @ c.T, median of 5 after 2 warm-ups: {cdt * 1000:.2f} ms",
         }
+    return line
+
+
+def root_merge_line(reps=10, warm=2, shards=8):
+    """configs[4]'s root merge at full size: rank 0's k-way
+    merge of the 8 gathered per-shard top-100 lists of 1M query rows, the one
+    piece of the 8-GPU step besides the RCCL gather that one GPU can time.
+    Input: the gather buffer [8][2][1M][100] (per shard an index plane and a
+    score plane) generated on device, each shard's list of a row sorted best
+    first (i.i.d. N(0,1) scores: the lists interleave as equal shards' top-k
+    do).  Timed with HIP events on the launch stream: the sorted-list merge the
+    sharded paths use (pmm_merge_sorted_topk_strided_device: prefixes first)
+    and the general merge (any list order) on the same buffer.  Algorithmic
+    bytes per launch (G + 1) M k 8: every list entry read once, the output
+    written once."""
+    import torch
+    from polars_matmul import _native
+
+    M, k, G = 1_000_000, 100, shards
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev)
+    g.manual_seed(42)
+    buf = torch.empty((G, 2, M, k), dtype=torch.int32, device=dev)
+    step = 1 << 17
+    for r0 in range(0, M, step):
+        r1 = min(M, r0 + step)
+        vals = torch.randn((G, r1 - r0, k), generator=g, device=dev)
+        vals, _ = torch.sort(vals, dim=2, descending=True)
+        buf[:, 1, r0:r1] = vals.view(torch.int32)
+        base = (torch.arange(G, device=dev, dtype=torch.int64) * 1_250_000).view(G, 1, 1)
+        ids = torch.randint(0, 1_250_000, (G, r1 - r0, k), generator=g, device=dev) + base
+        buf[:, 0, r0:r1] = ids.to(torch.int32)
+        del vals, ids
+    oi = torch.empty((M, k), dtype=torch.int32, device=dev)
+    osc = torch.empty((M, k), dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream()
+    out = {}
+    for name, srt in (("sorted", True), ("general", False)):
+        def run():
+            _native.merge_strided_device(buf.data_ptr(), buf[0, 1].data_ptr(), M, G, k, k, 2 * M * k, k,
+                                         _native.metric_from_str("cosine"), oi.data_ptr(), osc.data_ptr(),
+                                         stream=stream.cuda_stream, sorted_lists=srt)
+        for _ in range(warm):
+            run()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+        for i in range(reps):
+            ev[2 * i].record(stream)
+            run()
+            ev[2 * i + 1].record(stream)
+        torch.cuda.synchronize()
+        ms = sorted(ev[2 * i].elapsed_time(ev[2 * i + 1]) for i in range(reps))
+        avg = sum(ms) / reps
+        # spot check 4096 rows against torch over the concatenated lists
+        rows = torch.arange(0, M, M // 4096, device=dev)[:4096]
+        sc_all = buf[:, 1, rows].view(torch.float32).permute(1, 0, 2).reshape(len(rows), G * k)
+        id_all = buf[:, 0, rows].permute(1, 0, 2).reshape(len(rows), G * k)
+        ts, ti = torch.topk(sc_all, k, dim=1)
+        ok = bool(torch.equal(torch.gather(id_all, 1, ti), oi[rows])) and bool(torch.equal(ts, osc[rows]))
+        alg = (G + 1) * M * k * 8
+        out[name] = {"kernel_ms_avg": round(avg, 4), "kernel_ms_median": round(ms[reps // 2], 4),
+                     "achieved": round(alg / (avg / 1000.0) / 1e9, 1), "frac": round(alg / (avg / 1000.0) / 1e9 / HBM_PEAK_GBS, 4),
+                     "spot_check_4096_rows_exact": ok}
+    c = min(k, 256 // G)
+    line = {
+        "metric": f"root k-way merge of {G} x {M} x {k} sorted (index, score) lists", "unit": "GB/s",
+        "bound": "hbm", "peak": HBM_PEAK_GBS, "bytes_per_launch": (G + 1) * M * k * 8,
+        "kernel": "merge_kernel<1> (sorted: prefix fast path; general: every entry)",
+        "value": out["sorted"]["achieved"], "frac": out["sorted"]["frac"],
+        "kernel_ms_avg": out["sorted"]["kernel_ms_avg"],
+        "sorted_prefix_bytes_min": M * G * c * 8 + M * k * 8,
+        "sorted": out["sorted"], "general": out["general"],
+        "data": "device-generated: per shard and row 100 i.i.d. N(0,1) scores sorted best first, indices in the "
+                "shard's row range",
+    }
+    del buf, oi, osc
+    torch.cuda.empty_cache()
     return line
 
 
@@ -708,7 +823,11 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8, stride=1)
     seed_ms, _ = ks["seed"]
     all_gemm_ms = (gemm_ms or 0.0) + (seed_ms or 0.0)
     ms_step = elapsed / steps * 1000.0
-    ach = flops / (all_gemm_ms / 1000.0) / 1e12 if gemm_ms else None
+    # the dominant (fused) kernel alone: its algorithmic flops over its own
+    # average launch time (HIP events on its stream); the seed / prologue
+    # launch and the whole step are reported beside it, labelled
+    ach = flops / (gemm_ms / 1000.0) / 1e12 if gemm_ms else None
+    ach_seed = flops / (all_gemm_ms / 1000.0) / 1e12 if gemm_ms and seed_ms else None
     roof = {
         "bound": "mfma",
         "kernel": (BF16_KERNEL_NAMES[ks["bf16_kernel"]] if bf16 else
@@ -716,14 +835,17 @@ def measure(name, steps, warmup, rank, world, dist, dev, check_rows=8, stride=1)
         "achieved": round(ach, 2) if ach else None,
         "peak": peak, "unit": "TFLOP/s",
         "frac": round(ach / peak, 4) if ach else None,
+        "fused_frac": round(ach / peak, 4) if ach else None,
+        "with_seed_frac": round(ach_seed / peak, 4) if ach_seed else None,
         "traffic": traffic,
         "traffic_record": traffic_rec,
-        # per launch of the dominant kernel; a threshold-seeding pass
-        # (small problems only) is its own launch of the same
-        # kernel and is counted in "achieved"/"frac" too
+        # per launch of the dominant kernel; the threshold seed (small
+        # problems and bf16) is a launch of its own, counted
+        # only in "with_seed_frac" and "step_frac"
         "kernel_ms_avg": round(gemm_ms, 3) if gemm_ms else None,
         "kernel_launches_timed": ks["gemm"][1],
         "seed_ms_avg": round(seed_ms, 3) if seed_ms else None,
+        "seed_us": round(seed_ms * 1000.0, 2) if seed_ms else None,
         "flops_per_launch": flops,
         # the whole step (norms, fills, seed, GEMM, merge, gather) against the peak
         "step_frac": round(flops / (ms_step / 1000.0) / 1e12 / peak, 4),
@@ -1131,7 +1253,16 @@ def summary_of(line):
             b["materialised_ms"] = (rec.get("materialised") or {}).get("ms_per_step")
             out[name] = b
             continue
+        if name == "c5_root_merge":
+            out[name] = {"gbs": rec.get("value"), "frac": rec.get("frac"), "kernel_ms": rec.get("kernel_ms_avg"),
+                         "general_frac": (rec.get("general") or {}).get("frac")}
+            continue
         b = _brief(rec)
+        if rec.get("roofline", {}).get("step_frac") is not None and name in ("c1", "c2"):
+            b["step_frac"] = rec["roofline"]["step_frac"]
+            b["seed_us"] = rec["roofline"].get("seed_us")
+        if name == "matmul":
+            b["link_frac"] = rec.get("link_frac")
         if name == "c1" and isinstance(rec.get("boundary"), dict):
             b["e2e_ms"] = {leg: v["ms_per_call"] for leg, v in rec["boundary"].items()
                            if isinstance(v, dict) and "ms_per_call" in v}
@@ -1201,11 +1332,12 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="oracle baseline threads (0 = available_parallelism(), as faer's Rayon(0))")
     ap.add_argument("--boundary", type=int, default=1, help="also time the host-buffer C ABI (N=1)")
-    ap.add_argument("--extra", default="c4,c1,c2,c1_f64,f64_large,matmul,c5_rank",
+    ap.add_argument("--extra", default="c4,c1,c2,c1_f64,f64_large,matmul,c5_rank,c5_root_merge",
                     help="comma-separated secondary configs measured after the main line (N=1; 'none' = none; "
                          "'matmul' = .pmm.matmul at the c1 size; 'c1_f64' = the f64 top-k at the c1 size; "
                          "'f64_large' = the f64 top-k at 4096 x 1M x 256; 'c5_rank' = configs[4]'s per-GPU "
-                         "share, 1M x 1.25M x 1024, 1 warm-up + 2 timed steps)")
+                         "share, 1M x 1.25M x 1024, 1 warm-up + 2 timed steps; 'c5_root_merge' = configs[4]'s root "
+                         "merge of 8 x 1M x 100 gathered lists)")
     ap.add_argument("--metric", choices=("cosine", "dot", "euclidean"), default=None,
                     help="replace the main config's metric (the extras keep theirs)")
     ap.add_argument("--check", type=int, default=8, help="query rows spot-checked against an f64 top-k")
@@ -1327,6 +1459,7 @@ def main():
         for name in [x for x in args.extra.split(",") if x and x not in (args.config, "none")]:
             extra[name] = (matmul_line(args) if name == "matmul" else f64_line() if name == "c1_f64"
                            else f64_line(steps=3, warmup=1, large=True) if name == "f64_large"
+                           else root_merge_line() if name == "c5_root_merge"
                            else extra_line(name, args.steps, args.warmup, dev, args))
             log(f"extra {name}: {json.dumps(extra[name])}")
 

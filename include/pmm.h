@@ -231,9 +231,8 @@ int pmm_norms_f32_device(const float *a, int64_t ld, int64_t rows, int64_t d, in
 int pmm_norms_f64_device(const double *a, int64_t ld, int64_t rows, int64_t d, int squared,
                          double *out, void *stream);
 
-/* k-way merge of per-shard top-k lists: idx/score are [m][lists][k_in] (each
- * list best-first, as pmm_topk_f32_device writes them; idx 0xFFFFFFFF marks
- * an empty slot).  Writes the best k_out of each row to out_idx/out_score
+/* k-way merge of per-shard top-k lists: idx/score are [m][lists][k_in] (the
+ * lists in any order; idx 0xFFFFFFFF marks an empty slot).  Writes the best k_out of each row to out_idx/out_score
  * [m][k_out].  This is the merge step after the RCCL gather of the
  * corpus-sharded path (no reference counterpart: the reference is
  * single-process). */
@@ -252,6 +251,18 @@ int pmm_merge_topk_strided_device(const uint32_t *idx, const float *score, int64
                                   int64_t lists, int64_t k_in, int64_t row_stride,
                                   int64_t list_stride, int64_t k_out, int metric,
                                   uint32_t *out_idx, float *out_score, void *stream);
+
+/* The same merge of lists that are each best-first under the total order
+ * (score, then lower index; empty slots last) -- as every pmm_topk_* and merge
+ * output is.  A row's answer is then a prefix of each list: the kernel reads
+ * the first 256 / lists entries of each and reads on only for a row whose
+ * prefixes cannot hold its k_out best (lists <= 64, k_out <= 256; otherwise
+ * the general merge).  Unsorted input gives unspecified results.  The
+ * sharded paths (in-process and RCCL) merge with this entry. */
+int pmm_merge_sorted_topk_strided_device(const uint32_t *idx, const float *score, int64_t m,
+                                         int64_t lists, int64_t k_in, int64_t row_stride,
+                                         int64_t list_stride, int64_t k_out, int metric,
+                                         uint32_t *out_idx, float *out_score, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Device-resident corpus: upload a corpus once and run many top-k calls

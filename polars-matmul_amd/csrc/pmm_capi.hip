@@ -1178,6 +1178,7 @@ int topk_f32_host_chunked(const float *q, int64_t m, const float *c, int64_t n, 
   ma.list_stride = 2 * m * k;
   ma.M = (int)m;
   ma.S = kChunks;
+  ma.sorted = 1;  // each chunk's lists are a top-k output: best first
   ma.k_out = (int)k;
   ma.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
   ma.metric = metric;
@@ -1417,6 +1418,7 @@ int topk_sharded(const float *q, int64_t m, int64_t d, int64_t k, int metric, in
   ma.list_stride = 2 * m * k;
   ma.M = (int)m;
   ma.S = G;
+  ma.sorted = 1;  // each shard's lists are a top-k output: best first
   ma.k_out = (int)k;
   ma.P = std::min(8192, next_pow2(2 * (int)k + 64, 128));
   ma.metric = metric;
@@ -2159,10 +2161,29 @@ int pmm_merge_topk_device(const uint32_t *idx, const float *score, int64_t m, in
                                        out_idx, out_score, stream);
 }
 
+static int merge_strided(const uint32_t *idx, const float *score, int64_t m, int64_t lists, int64_t k_in,
+                         int64_t row_stride, int64_t list_stride, int64_t k_out, int metric, uint32_t *out_idx,
+                         float *out_score, void *stream, bool sorted);
+
 int pmm_merge_topk_strided_device(const uint32_t *idx, const float *score, int64_t m,
                                   int64_t lists, int64_t k_in, int64_t row_stride,
                                   int64_t list_stride, int64_t k_out, int metric,
                                   uint32_t *out_idx, float *out_score, void *stream) {
+  return merge_strided(idx, score, m, lists, k_in, row_stride, list_stride, k_out, metric, out_idx, out_score,
+                       stream, false);
+}
+
+int pmm_merge_sorted_topk_strided_device(const uint32_t *idx, const float *score, int64_t m,
+                                         int64_t lists, int64_t k_in, int64_t row_stride,
+                                         int64_t list_stride, int64_t k_out, int metric,
+                                         uint32_t *out_idx, float *out_score, void *stream) {
+  return merge_strided(idx, score, m, lists, k_in, row_stride, list_stride, k_out, metric, out_idx, out_score,
+                       stream, true);
+}
+
+static int merge_strided(const uint32_t *idx, const float *score, int64_t m, int64_t lists, int64_t k_in,
+                         int64_t row_stride, int64_t list_stride, int64_t k_out, int metric, uint32_t *out_idx,
+                         float *out_score, void *stream, bool sorted) {
   int rc;
   if ((rc = check_metric(metric))) return rc;
   if (m < 0 || lists < 1 || k_in < 0 || k_out < 0 || k_out > lists * k_in || row_stride < 0 ||
@@ -2182,6 +2203,7 @@ int pmm_merge_topk_strided_device(const uint32_t *idx, const float *score, int64
   ma.list_stride = list_stride;
   ma.M = (int)m;
   ma.S = (int)lists;
+  ma.sorted = sorted ? 1 : 0;
   ma.k_out = (int)k_out;
   ma.P = std::min(8192, next_pow2(2 * (int)k_out + 64, 128));
   ma.metric = metric;

@@ -93,6 +93,7 @@ struct MergeArgs {
   int ablate;  // benchmarking only (PMM_MERGE_ABLATE): 1 = no selection/sort, 2 = no candidate loads
   int no_rank;  // set by launch_merge: bitonic sort instead of rank counting (many rows)
   int flags;    // set by launch_merge: kMergeReverse, kMergePipelined, kMergeSplitRow
+  int sorted;   // loader 1: every input list is best-first (the prefix fast path)
 };
 constexpr int kMergeReverse = 1;    // rows last to first (split rows, the heavy ones, start first)
 constexpr int kMergePipelined = 2;  // next candidate batch's loads in flight while one is taken

@@ -895,21 +895,29 @@ __device__ inline void wave_rank2(u64 y0, u64 y1, int n, int &r0, int &r1) {
     r1 += v > y1;
   }
 }
-// the k best of the cnt (<= 64 E) keys in scr, unordered, to its front
+// the k best of the cnt (<= 64 E) keys in scr, unordered, to its front.
+// The raised threshold comes back by value with the count: a threshold the
+// callee wrote through a pointer lived in scratch memory, and every scratch
+// read of it (one per taken batch) waited for the batch loads in flight
+// (scratch counts in vmcnt).
+struct CompactOut {
+  int cnt;
+  u64 T;
+};
 template <int E>
-__device__ inline int merge_select(u64 *scr, int cnt, int k, u64 *T, int lane) {
+__device__ inline CompactOut merge_select(u64 *scr, int cnt, int k, u64 T, int lane) {
   u64 x[E];
 #pragma unroll
   for (int e = 0; e < E; e++) x[e] = (lane + 64 * e < cnt) ? scr[MP(lane + 64 * e)] : 0ull;
   wave_sync();  // every lane has read before any rewrites
   const u64 t = wave_kth_u64<E>(x, k);
-  if (t > *T) *T = t;
+  if (t > T) T = t;
   cnt = wave_keep_ge<E>(x, t, [&](int pos, u64 v) __attribute__((always_inline)) { scr[MP(pos)] = v; }, lane);
   wave_sync();
-  return cnt;
+  return {cnt, T};
 }
 
-__device__ int merge_compact(u64 *scr, int cnt, int k, int P, u64 *T, int lane) {
+__device__ CompactOut merge_compact(u64 *scr, int cnt, int k, int P, u64 T, int lane) {
   if (P <= 512 && cnt > k) {
     // select the k best (wave_kth_u64) over as few key slots per lane as
     // hold cnt: its cost is a compare per slot per bit
@@ -924,18 +932,16 @@ __device__ int merge_compact(u64 *scr, int cnt, int k, int P, u64 *T, int lane) 
   wave_sort_desc_u64_pad(scr, P, lane);
   if (cnt >= k) {
     const u64 t = scr[MP(k - 1)];
-    if (t > *T) *T = t;
+    if (t > T) T = t;
     cnt = k;
   }
   wave_sync();
-  return cnt;
+  return {cnt, T};
 }
 
-template <int LOADER, bool SPLIT>
-__global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wpb = blockDim.x >> 6;
+template <int LOADER, bool SPLIT, bool SORTED>
+__device__ __forceinline__ void merge_row(const MergeArgs &a, const int rpos, const int wid, const int lane,
+                                          char *smem) {
   // kMergeSplitRow (few rows, many lists, k <= 64): the block's 4 waves take
   // one row, wave w merging lists [S w / 4, S (w + 1) / 4) down to its k best;
   // wave 0 then selects the row's k best of those 4 lists.  Otherwise one
@@ -944,8 +950,6 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   // (a template parameter: the one-wave-per-row instantiation keeps its
   // registers -- a runtime flag cost it an occupancy step, c3 0.57 vs 0.44 ms)
   constexpr bool split = SPLIT;
-  const int rpos = split ? (int)blockIdx.x : (int)blockIdx.x * wpb + wid;
-  if (rpos >= a.M) return;  // whole wave exits
   // kMergeReverse: the split units' rows (many segments each) sit after the
   // whole query blocks' rows (one segment); started first, the long rows no
   // longer form the launch's tail
@@ -960,8 +964,8 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     const int64_t off = (int64_t)row * a.row_stride + (int64_t)s * a.list_stride + i;
     const uint32_t id = a.in_idx[off];
     const float sc = a.in_score[off];
-    return id != 0xFFFFFFFFu ? ((u64)okey32(a.metric == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~id)
-                             : 0ull;
+    const u64 key = ((u64)okey32(a.metric == kMetricEuclidean ? -sc : sc) << 32) | (u64)(~id);
+    return id != 0xFFFFFFFFu ? key : 0ull;
   };
   auto take = [&](u64 x) __attribute__((always_inline)) {
     const bool keep = (x != 0ull) && (x >= T);
@@ -971,11 +975,46 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     cnt += __popcll(m);
     if (cnt > a.P - 64) {
       wave_sync();
-      cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
+      {
+        const CompactOut o = merge_compact(scr, cnt, a.k_out, a.P, T, lane);
+        cnt = o.cnt;
+        T = o.T;
+      }
     }
   };
-  if (PMM_ABL(a.ablate) == 2) {
-    // (benchmarking only: no candidate loads)
+  bool done = false;
+  if (SORTED) {
+    const int c = min(a.k_in, 256 / a.S);  // prefix read per list (launch_merge: S <= 64)
+    const int n = a.S * c;
+    u64 x[4];
+    u64 ul = 0ull;  // this lane's last-read entries of lists not read to the end
+    // (loads unconditional from clamped positions, keys selected: no load
+    // under a branch, so the four are in flight together)
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int f = j * 64 + lane;
+      const bool valid = f < n;
+      const int g = valid ? f / c : 0, i = valid ? f - g * c : 0;
+      const u64 v = load_x(g, i);
+      x[j] = valid ? v : 0ull;
+      if (valid && i == c - 1 && c < a.k_in && v > ul) ul = v;
+    }
+    const u64 U = wave_max_u64(ul);
+    int nge = 0, nz = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      nge += __popcll(__ballot(x[j] != 0ull && x[j] >= U));
+      nz += __popcll(__ballot(x[j] != 0ull));
+    }
+    if (nge >= a.k_out || (U == 0ull)) {
+      // (U == 0: every list read to its end, or its unread part empty slots)
+      const u64 t = nz > a.k_out ? wave_kth_u64<4>(x, a.k_out) : 1ull;
+      cnt = wave_keep_ge<4>(x, t, [&](int pos, u64 v) __attribute__((always_inline)) { scr[MP(pos)] = v; }, lane);
+      done = true;
+    }
+  }
+  if (done || PMM_ABL(a.ablate) == 2) {
+    // (ablate 2, benchmarking only: no candidate loads)
   } else if (a.S <= 64) {
     // All list lengths in one load (lane s holds list s's), then the lists'
     // 64-entry chunks as one flat sequence, MU chunk loads in flight at a
@@ -994,13 +1033,21 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
       s++;
       ns = (s < s_hi) ? __builtin_amdgcn_readlane(nl, s - s_lo) : 0;
     }
-    auto fetch = [&](u64(&x)[MU]) __attribute__((always_inline)) {
+    // A batch: the positions of its MU chunks first (scalar bookkeeping),
+    // then MU loads with no branch around them, each from its position or,
+    // past the lists, from a valid dummy one, flagged invalid; the flag is
+    // applied where the key is taken.  (A load under a branch, or a register
+    // a load is still filling copied at a branch join, waits for the load
+    // there: round 5's batches did both, so each batch paid a full memory
+    // latency before the next went out.)
+    auto fetch = [&](u64(&x)[MU], bool(&vx)[MU]) __attribute__((always_inline)) {
+      int ps[MU], pc[MU], pn[MU];
 #pragma unroll
       for (int u = 0; u < MU; u++) {
-        x[u] = 0ull;
+        ps[u] = s;
+        pc[u] = c;
+        pn[u] = (s < s_hi) ? ns : 0;
         if (s < s_hi) {
-          const int i = c + lane;
-          if (i < ns) x[u] = load_x(s, i);
           c += 64;
           while (s < s_hi && c >= ns) {
             s++;
@@ -1009,29 +1056,41 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
           }
         }
       }
+#pragma unroll
+      for (int u = 0; u < MU; u++) {
+        const int i = pc[u] + lane;
+        vx[u] = i < pn[u];
+        x[u] = load_x(vx[u] ? ps[u] : s_lo, vx[u] ? i : 0);
+      }
     };
     if (a.flags & kMergePipelined) {
       // the next batch's loads go out before this one is taken (a row's
-      // batches no longer pay one memory latency each)
+      // batches no longer pay one memory latency each); two register sets
+      // in turn, never copied into each other
       if (s < s_hi) {
         u64 x[MU], y[MU];
-        fetch(x);
+        bool vx[MU], vy[MU];
+        fetch(x, vx);
         for (;;) {
-          const bool more = s < s_hi;
-          if (more) fetch(y);
+          bool more = s < s_hi;
+          if (more) fetch(y, vy);
 #pragma unroll
-          for (int u = 0; u < MU; u++) take(x[u]);
+          for (int u = 0; u < MU; u++) take(vx[u] ? x[u] : 0ull);
           if (!more) break;
+          more = s < s_hi;
+          if (more) fetch(x, vx);
 #pragma unroll
-          for (int u = 0; u < MU; u++) x[u] = y[u];
+          for (int u = 0; u < MU; u++) take(vy[u] ? y[u] : 0ull);
+          if (!more) break;
         }
       }
     } else {
       while (s < s_hi) {
         u64 x[MU];
-        fetch(x);
+        bool vx[MU];
+        fetch(x, vx);
 #pragma unroll
-        for (int u = 0; u < MU; u++) take(x[u]);
+        for (int u = 0; u < MU; u++) take(vx[u] ? x[u] : 0ull);
       }
     }
   } else {
@@ -1060,7 +1119,11 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
   if (split) {
     // each wave's k best (k <= 64: one slot per lane), then wave 0 takes the
     // row's k best of the four lists into its own scratch
-    if (cnt > a.k_out) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
+    if (cnt > a.k_out) {
+        const CompactOut o = merge_compact(scr, cnt, a.k_out, a.P, T, lane);
+        cnt = o.cnt;
+        T = o.T;
+      }
     int *cnts = (int *)((u64 *)smem + (size_t)4 * MPN(a.P));
     if (lane == 0) cnts[wid] = cnt;
     __syncthreads();
@@ -1079,7 +1142,11 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     wave_sync();
   }
   if (PMM_ABL(a.ablate) != 1) {
-    if (cnt > a.k_out && a.P <= 512) cnt = merge_compact(scr, cnt, a.k_out, a.P, &T, lane);
+    if (cnt > a.k_out && a.P <= 512) {
+        const CompactOut o = merge_compact(scr, cnt, a.k_out, a.P, T, lane);
+        cnt = o.cnt;
+        T = o.T;
+      }
     if (a.k_out <= 128 && cnt <= a.k_out && !a.no_rank) {
       // best-first by rank counting, no sort: each kept key goes to the
       // position = the number of kept keys above it (keys are distinct)
@@ -1098,6 +1165,136 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
     wave_sort_desc_u64_pad(scr, P2, lane);
   }
   for (int j = lane; j < a.k_out; j += 64) put(j, (j < cnt) ? scr[MP(j)] : 0ull);
+}
+
+template <int LOADER, bool SPLIT, bool SORTED = false>
+__global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wpb = blockDim.x >> 6;
+  const int rpos = SPLIT ? (int)blockIdx.x : (int)blockIdx.x * wpb + wid;
+  if (rpos >= a.M) return;  // whole wave exits
+  merge_row<LOADER, SPLIT, SORTED>(a, rpos, wid, lane, smem);
+}
+
+// ===========================================================================
+// k-way merge of 5..8 sorted lists per row (loader 1, MergeArgs::sorted: the
+// root merge of the corpus-sharded path, configs[4]).  Eight rows per wave,
+// eight lanes per row, lane g of a row holding list g: the first kKwayP
+// entries of every list are staged in LDS as composite keys (coalesced: 32
+// lanes read one list's 128 contiguous bytes per plane), then k_out steps of
+// a true merge -- the row's largest head by three DPP max steps inside the
+// 8-lane group, its list advances, the group's first lane writes the entry.
+// A list that would need entries past its staged prefix (its share of the
+// answer exceeds kKwayP: skewed shards) marks its row, which the wave then
+// merges again by the general path (merge_row) over every entry.  ~30 vector
+// instructions per step for 8 rows at once, no selection and no sort: the
+// lists' order is the merge's order.
+// ===========================================================================
+constexpr int kKwayP = 32;  // staged entries per (row, list), the largest instantiation
+__device__ __forceinline__ u64 dpp_u64(u64 v, int ctrl_sel) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  if (ctrl_sel == 0) {  // row_half_mirror: lane i of each 8 <- lane 7 - i
+    lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x141, 0xF, 0xF, false);
+    hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x141, 0xF, 0xF, false);
+  } else if (ctrl_sel == 1) {  // quad_perm [2,3,0,1]: lane xor 2
+    lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x4E, 0xF, 0xF, false);
+    hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x4E, 0xF, 0xF, false);
+  } else {  // quad_perm [1,0,3,2]: lane xor 1
+    lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false);
+    hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false);
+  }
+  return ((u64)hi << 32) | lo;
+}
+template <int KP>
+__global__ __launch_bounds__(256) void kway_merge_kernel(MergeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int kKwayP = KP;
+  u64 *st = (u64 *)smem + (size_t)wid * 64 * kKwayP;  // [segment 8 r + g][kKwayP]
+  const int row0 = ((int)blockIdx.x * (int)(blockDim.x >> 6) + wid) * 8;
+  if (row0 >= a.M) return;  // whole wave exits
+  const int lim = min(kKwayP, a.k_in);
+  // stage: iteration t, lanes 32 h .. 32 h + 31 take entries 0..31 of
+  // segment 2 t + h (row row0 + s / 8, list s % 8)
+  // (loads unconditional, from a clamped offset, and the key selected: a
+  // load under a branch waits for its data before the next is issued)
+  // (all of a batch's loads first, then its LDS stores: the LDS pointer is
+  // generic, so a load may not pass an earlier store)
+  static_assert(KP <= 32, "staged prefix: one lane per entry");
+  for (int t0 = 0; t0 < 32; t0 += 8) {  // (64 segments, two per iteration)
+    uint32_t id[8];
+    float sc[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int sg = 2 * (t0 + u) + (lane >> 5), e = lane & 31;
+      const int r = sg >> 3, g = sg & 7, row = row0 + r;
+      const bool valid = row < a.M && g < a.S && e < lim;  // (e >= KP: lim <= KP)
+      const int64_t off = valid ? (int64_t)row * a.row_stride + (int64_t)g * a.list_stride + e : 0;
+      id[u] = a.in_idx[off];
+      sc[u] = a.in_score[off];
+      if (!valid) id[u] = 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int sg = 2 * (t0 + u) + (lane >> 5), e = lane & 31;
+      const u64 key = ((u64)okey32(a.metric == kMetricEuclidean ? -sc[u] : sc[u]) << 32) | (u64)(~id[u]);
+      if (e < KP) st[sg * kKwayP + e] = id[u] != 0xFFFFFFFFu ? key : 0ull;
+    }
+  }
+  wave_sync();
+  const int r = lane >> 3, row = row0 + r;
+  const u64 *mine = st + lane * kKwayP;
+  int ptr = 0;
+  u64 h = mine[0];
+  bool fail = false;
+  const bool writer = (lane & 7) == 0 && row < a.M;
+  uint32_t *oi = a.out_idx + (int64_t)row * a.k_out;
+  float *os = a.out_score + (int64_t)row * a.k_out;
+  for (int j = 0; j < a.k_out; j++) {
+    u64 m = h, o;
+    o = dpp_u64(m, 0);
+    m = o > m ? o : m;
+    o = dpp_u64(m, 1);
+    m = o > m ? o : m;
+    o = dpp_u64(m, 2);
+    m = o > m ? o : m;
+    // the group's winner: its lowest lane holding the maximum (equal keys,
+    // which distinct shard indices never give, would come from the lower list first)
+    const u64 eq = __ballot(m != 0ull && h == m);
+    const uint32_t grp = (uint32_t)(eq >> (lane & ~7)) & 0xFFu;
+    if (grp != 0u && (lane & 7) == __builtin_ctz(grp)) {
+      ptr++;
+      if (ptr >= lim && ptr < a.k_in) fail = true;  // the next entry is past the staged prefix
+      h = ptr < lim ? mine[ptr] : 0ull;
+    }
+    if (writer) {
+      uint32_t id = 0xFFFFFFFFu;
+      float sc = __uint_as_float(0x7FC00000u);
+      if (m != 0ull) {
+        id = ~(uint32_t)m;
+        const float v = dekey32((uint32_t)(m >> 32));
+        sc = (a.metric == kMetricEuclidean) ? 0.0f - v : v;
+      }
+      oi[j] = id;
+      os[j] = sc;
+    }
+  }
+  // rows a skewed list made fail: the general path over every entry (the
+  // staging area is the scratch now; its stores land after the ones above)
+  u64 fm = __ballot(fail);
+  if (fm) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_sync();
+    MergeArgs b = a;
+    b.flags &= ~kMergeReverse;  // (merge_row's rpos is the row itself)
+    while (fm) {
+      const int rr = __builtin_ctzll(fm) >> 3;
+      fm &= ~(0xFFull << (8 * rr));
+      merge_row<1, false, false>(b, row0 + rr, wid, lane, (char *)st - (size_t)wid * MPN(a.P) * 8);
+      wave_sync();
+    }
+  }
 }
 
 size_t merge_lds_bytes_per_wave(int P) { return (size_t)MPN(P) * 8; }
@@ -1857,7 +2054,32 @@ hipError_t launch_merge(const MergeArgs &a0, int loader, hipStream_t s) {
   // four waves per row where rows are few and each has many lists to merge
   // (c1: 1000 rows x 27 lists, one wave per SIMD otherwise) and the per-wave
   // lists fit one slot per lane (k <= 64)
-  if (!(a.S >= 8 && a.k_out <= 64 && a.P <= 512 && !a.no_rank && a.ablate == 0)) a.flags &= ~kMergeSplitRow;
+  // sorted input lists (loader 1, MergeArgs::sorted): the prefix fast path
+  // when the prefixes can hold the answer (c = 256 / S >= 1 entries per list
+  // and k_out <= 256); one wave per row
+  const bool sorted = loader == 1 && a.sorted && a.S <= 64 && a.k_out <= 256 && a.P <= 512 &&
+                      !(getenv("PMM_MERGE_SORTED") && atoi(getenv("PMM_MERGE_SORTED")) == 0);
+  // 5..8 sorted lists (the 8-GPU root merge): the k-way kernel, 8 rows per
+  // wave (PMM_MERGE_KWAY=0: the prefix fast path instead)
+  if (sorted && a.S >= 5 && a.S <= 8 && a.k_out <= 8 * kKwayP &&
+      !(getenv("PMM_MERGE_KWAY") && atoi(getenv("PMM_MERGE_KWAY")) == 0) &&
+      (size_t)MPN(a.P) * 8 <= (size_t)64 * kKwayP * 8) {
+    // (PMM_KWAY_P = 24 / PMM_KWAY_WPB = 4: A/B knobs -- fewer staged
+    // entries per list, more waves per block)
+    static const int kp = getenv("PMM_KWAY_P") ? atoi(getenv("PMM_KWAY_P")) : 32;
+    static const int wpb = getenv("PMM_KWAY_WPB") ? atoi(getenv("PMM_KWAY_WPB")) : 2;
+    const int rows_per_block = 8 * wpb;
+    const unsigned grid = (unsigned)((a.M + rows_per_block - 1) / rows_per_block);
+    if (kp == 24 && (size_t)MPN(a.P) * 8 <= (size_t)64 * 24 * 8) {
+      if (wpb == 4) (void)hipFuncSetAttribute((const void *)kway_merge_kernel<24>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      kway_merge_kernel<24><<<grid, 64 * wpb, (size_t)wpb * 64 * 24 * 8, s>>>(a);
+    } else {
+      if (wpb == 4) (void)hipFuncSetAttribute((const void *)kway_merge_kernel<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      kway_merge_kernel<32><<<grid, 64 * wpb, (size_t)wpb * 64 * 32 * 8, s>>>(a);
+    }
+    return hipGetLastError();
+  }
+  if (!(a.S >= 8 && a.k_out <= 64 && a.P <= 512 && !a.no_rank && a.ablate == 0) || sorted) a.flags &= ~kMergeSplitRow;
   const bool split = (a.flags & kMergeSplitRow) != 0;
   int wpb = (int)(65536 / merge_lds_bytes_per_wave(a.P));
   wpb = split ? 4 : (wpb < 1 ? 1 : (wpb > 4 ? 4 : wpb));
@@ -1872,7 +2094,9 @@ hipError_t launch_merge(const MergeArgs &a0, int loader, hipStream_t s) {
       attr_set[loader] = true;
     }
   }
-  if (split) {
+  if (sorted) {
+    merge_kernel<1, false, true><<<grid, wpb * 64, lds, s>>>(a);
+  } else if (split) {
     if (loader == 0) merge_kernel<0, true><<<grid, wpb * 64, lds, s>>>(a);
     else merge_kernel<1, true><<<grid, wpb * 64, lds, s>>>(a);
   } else {

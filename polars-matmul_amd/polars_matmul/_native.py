@@ -64,6 +64,7 @@ EXPORTED_SYMBOLS = (
     "pmm_topk_bf16_device",
     "pmm_merge_topk_device",
     "pmm_merge_topk_strided_device",
+    "pmm_merge_sorted_topk_strided_device",
     "pmm_norms_f32_device",
     "pmm_norms_f64_device",
     "pmm_corpus_create_f32",
@@ -149,6 +150,8 @@ _SIGS = {
     ),
     "pmm_merge_topk_device": ([_vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp], _i32),
     "pmm_merge_topk_strided_device": (
+        [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp], _i32),
+    "pmm_merge_sorted_topk_strided_device": (
         [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _vp, _vp, _vp], _i32),
     "pmm_norms_f32_device": ([_vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
     "pmm_norms_f64_device": ([_vp, _i64, _i64, _i64, _i32, _vp, _vp], _i32),
@@ -459,10 +462,14 @@ def merge_device(idx_ptr: int, score_ptr: int, m: int, lists: int, k_in: int, k_
 
 def merge_strided_device(idx_ptr: int, score_ptr: int, m: int, lists: int, k_in: int,
                          row_stride: int, list_stride: int, k_out: int, metric: int,
-                         out_idx_ptr: int, out_score_ptr: int, stream: int = 0) -> None:
-    check(_lib.pmm_merge_topk_strided_device(idx_ptr, score_ptr, m, lists, k_in, row_stride,
-                                             list_stride, k_out, metric, out_idx_ptr,
-                                             out_score_ptr, stream or None))
+                         out_idx_ptr: int, out_score_ptr: int, stream: int = 0, *,
+                         sorted_lists: bool = False) -> None:
+    """k-way merge of strided lists; sorted_lists=True: every list is
+    best-first (a top-k or merge output), so the prefix fast path applies
+    (pmm_merge_sorted_topk_strided_device)."""
+    fn = _lib.pmm_merge_sorted_topk_strided_device if sorted_lists else _lib.pmm_merge_topk_strided_device
+    check(fn(idx_ptr, score_ptr, m, lists, k_in, row_stride, list_stride, k_out, metric, out_idx_ptr,
+             out_score_ptr, stream or None))
 
 
 def norms_device(a_ptr: int, ld: int, rows: int, d: int, squared: bool, out_ptr: int, *,

@@ -74,13 +74,15 @@ def _device_merge(gathered: torch.Tensor, k: int, metric: int, out_i: torch.Tens
                   out_s: torch.Tensor) -> None:
     """k-way merge of the gathered [world][2][M][k_in] lists (per rank: an
     index plane, then a score plane) in place, with no re-layout copy
-    (pmm_merge_topk_strided_device)."""
+    (pmm_merge_sorted_topk_strided_device: every rank's lists are its top-k,
+    best first, so each row reads only the prefixes that can hold its answer)."""
     from . import _native
 
     world, _, m, kin = gathered.shape
     _native.merge_strided_device(gathered.data_ptr(), gathered[0, 1].data_ptr(), m, world, kin,
                                  kin, 2 * m * kin, k, metric, out_i.data_ptr(), out_s.data_ptr(),
-                                 stream=torch.cuda.current_stream(gathered.device).cuda_stream)
+                                 stream=torch.cuda.current_stream(gathered.device).cuda_stream,
+                                 sorted_lists=True)
 
 
 class ShardedTopK:

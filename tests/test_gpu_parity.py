@@ -553,6 +553,69 @@ def test_merge_random_lists(m, lists, k_in, k_out, metric, empty, tied):
         assert np.all(gi[r, nv:] == 0xFFFFFFFF) and np.all(np.isnan(gsc[r, nv:])), f"row {r}"
 
 
+# ---- the sorted-list merge (pmm_merge_sorted_topk_strided_device: each
+# list best-first, as every top-k output is; the prefix fast path, with the
+# general path for rows whose prefixes cannot hold the answer) against the
+# general merge and NumPy, in the [lists][2][m][k_in] layout of the gather ----
+@pytest.mark.parametrize("m,lists,k_in,k_out,metric,empty,tied,skew", [
+    (3000, 8, 100, 100, 0, 0.0, False, "none"), (3000, 8, 100, 100, 2, 0.0, True, "none"),
+    (500, 8, 100, 100, 1, 0.0, False, "one"), (500, 8, 100, 100, 0, 0.0, False, "two"),
+    (400, 2, 300, 256, 0, 0.1, False, "none"), (400, 3, 40, 100, 1, 0.5, False, "none"),
+    (400, 16, 64, 100, 0, 0.05, True, "none"), (200, 64, 10, 64, 2, 0.0, False, "none"),
+    (200, 70, 8, 100, 0, 0.0, False, "none"), (200, 8, 50, 300, 1, 0.0, False, "none"),
+    (300, 1, 120, 100, 0, 0.2, True, "none"), (300, 5, 7, 30, 0, 0.0, False, "none"),
+    (300, 6, 40, 200, 2, 0.1, False, "none"), (300, 7, 20, 100, 0, 0.0, True, "none"),
+    (70000, 8, 100, 100, 0, 0.0, False, "none")])
+def test_merge_sorted_lists(m, lists, k_in, k_out, metric, empty, tied, skew):
+    import torch
+    n = _native()
+    rs = np.random.RandomState(m + lists * 7 + k_in * 3 + k_out)
+    # distinct global indices per row (shard g's rows are [g * 2^20, (g + 1) * 2^20))
+    idx = np.stack([np.concatenate([g * (1 << 20) + rs.permutation(1 << 12)[:k_in] for g in range(lists)])
+                    for _ in range(m)]).reshape(m, lists, k_in).astype(np.uint32)
+    sc = (rs.randint(0, 40, size=idx.shape) / 40.0 if tied else rs.randn(*idx.shape)).astype(np.float32)
+    if skew == "one":    # every row's answer from list 0 (the prefixes cannot hold it)
+        sc[:, 0] += 10.0
+    elif skew == "two":  # lists 0 and 1 dominate
+        sc[:, :2] += 10.0
+    if metric == 2:
+        sc = np.abs(sc) if skew == "none" else np.abs(sc - 20.0)
+    drop = rs.rand(*idx.shape) < empty
+    idx[drop] = 0xFFFFFFFF
+    sc[drop] = np.nan
+    # best first under the total order: score (desc; euclidean asc), then lower index; empty slots last
+    for r in range(m):
+        for g in range(lists):
+            ii, ss = idx[r, g], sc[r, g]
+            key = np.where(ii == 0xFFFFFFFF, np.inf, -ss if metric != 2 else ss)
+            o = np.lexsort((ii, key))
+            idx[r, g], sc[r, g] = ii[o], ss[o]
+    dev = torch.device("cuda:0")
+    buf = torch.empty((lists, 2, m, k_in), dtype=torch.int32, device=dev)
+    buf[:, 0] = torch.from_numpy(np.ascontiguousarray(idx.transpose(1, 0, 2)).view(np.int32)).to(dev)
+    buf[:, 1] = torch.from_numpy(np.ascontiguousarray(sc.transpose(1, 0, 2)).view(np.int32)).to(dev)
+    outs = {}
+    for srt in (False, True):
+        oi = torch.full((m, k_out), 7, dtype=torch.int32, device=dev)
+        os_ = torch.full((m, k_out), 7.0, dtype=torch.float32, device=dev)
+        n.merge_strided_device(buf.data_ptr(), buf[0, 1].data_ptr(), m, lists, k_in, k_in, 2 * m * k_in, k_out,
+                               metric, oi.data_ptr(), os_.data_ptr(), sorted_lists=srt)
+        torch.cuda.synchronize()
+        outs[srt] = (oi.cpu().numpy().view(np.uint32), os_.cpu().numpy())
+    assert np.array_equal(outs[True][0], outs[False][0])
+    assert np.array_equal(outs[True][1].view(np.uint32), outs[False][1].view(np.uint32))
+    gi, gsc = outs[True]
+    fi_all, fs_all = idx.reshape(m, -1), sc.reshape(m, -1)
+    for r in range(0, m, max(1, m // 50)):
+        ok = fi_all[r] != 0xFFFFFFFF
+        fi, fs = fi_all[r][ok], fs_all[r][ok]
+        order = np.lexsort((fi, fs if metric == 2 else -fs))[:k_out]
+        nv = len(order)
+        assert np.array_equal(gi[r, :nv], fi[order]), f"row {r}"
+        assert np.array_equal(gsc[r, :nv], fs[order]), f"row {r}"
+        assert np.all(gi[r, nv:] == 0xFFFFFFFF) and np.all(np.isnan(gsc[r, nv:])), f"row {r}"
+
+
 def test_c5_shape_corpus_sharded_8way(pmm):
     # BASELINE configs[4] (1M x 10M x 1024 cosine k=100 on 8 GPUs, corpus
     # row-sharded) at a size one GPU checks in seconds: D = 1024, k = 100,
