@@ -1161,7 +1161,11 @@ def run_inproc_child(args, world, spawner):
                          "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "TORCHELASTIC_RUN_ID")}
     cmd = [sys.executable, os.path.abspath(__file__), "--inproc-child", str(world), "--config", args.config,
            "--steps", str(args.steps), "--warmup", str(args.warmup)] + (["--metric", args.metric] if args.metric else [])
-    r = spawner.run(cmd, env, args.inproc_timeout)
+    # (c5's child synthesises a 40 GB host corpus, uploads it sharded and runs
+    # ~18 s steps: a longer limit for problems of that size)
+    M, N, D = CONFIGS[args.config][:3]
+    timeout = args.inproc_timeout if args.inproc_timeout > 0 else (900 if M * N * D > 1e15 else 300)
+    r = spawner.run(cmd, env, timeout)
     lines = [x for x in r["stdout"].splitlines() if x.startswith("{")]
     if r["rc"] != 0 or not lines:
         return {"error": f"in-process child rc={r['rc']}", "stderr_tail": r["stderr"][-800:]}
@@ -1348,7 +1352,7 @@ def main():
     ap.add_argument("--inproc", type=int, default=1,
                     help="N > 1: after the RCCL ranks, also measure the in-process transport (one child "
                          "process driving all N GPUs through pmm_set_devices) under extra.inproc")
-    ap.add_argument("--inproc-timeout", type=int, default=300, help=argparse.SUPPRESS)
+    ap.add_argument("--inproc-timeout", type=int, default=0, help=argparse.SUPPRESS)  # 0: by problem size
     ap.add_argument("--inproc-child", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.metric and args.metric != CONFIGS[args.config][4]:

@@ -93,8 +93,12 @@ int pmm_set_device(int device);
  * threshold seed run, so near-ties may resolve differently than on one device
  * (tests assert > 99% index agreement).  A device may be listed more than once
  * (one shard per entry).  A one-entry list moves every host call to that
- * device.  Work that is not sharded (f64, k > 1024, pmm_matmul_*) runs on
- * ids[0].  Process-wide; n = 0 (or ids = NULL) returns to one device
+ * device.  The f64 entries (pmm_topk_f64, pmm_corpus_create_f64 /
+ * pmm_topk_f64_corpus; any k) shard the same way: each device runs the f64
+ * top-k on its shard (k_g = min(k, shard rows), padded with empty slots), the
+ * [m][k] (index, f64 score) lists meet on ids[0] and are k-way merged there,
+ * bit-equal to one device (indices and f64 scores).  Work that is not sharded
+ * (f32 k > 1024, pmm_matmul_*) runs on ids[0].  Process-wide; n = 0 (or ids = NULL) returns to one device
  * (pmm_set_device's).
  * VERIFIED ON ONE GPU ONLY: the one-GPU test box lists device 0 repeatedly,
  * which plans all shards onto one stream; the distinct-device branch
@@ -283,8 +287,8 @@ typedef struct pmm_corpus pmm_corpus;
 
 int pmm_corpus_create_f32(const float *c, int64_t n, int64_t d, pmm_corpus **out);
 /* An f64 corpus: rows kept in f64 (stride roundup(d, 16), zero-padded) with
- * their f64 norms of both metrics, on ONE device (the device list's first
- * entry when pmm_set_devices is in effect: f64 work is not sharded). */
+ * their f64 norms of both metrics; with pmm_set_devices in effect, row-sharded
+ * over the list like an f32 corpus (pmm_topk_f64_corpus merges the shards). */
 int pmm_corpus_create_f64(const double *c, int64_t n, int64_t d, pmm_corpus **out);
 /* PMM_DTYPE_F32 or PMM_DTYPE_F64. */
 int pmm_corpus_dtype(const pmm_corpus *corpus, int *dtype);

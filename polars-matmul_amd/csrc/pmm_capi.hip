@@ -1552,9 +1552,13 @@ int topk_f64_materialised(const double *dq, int64_t ldq, int64_t m, const double
   return PMM_OK;
 }
 
+// flag_copy (the sharded path): instead of waiting here for the fused scan's
+// overflow flag, enqueue a copy of it to flag_copy (device memory) and return;
+// the caller checks it once every device has finished and re-runs an
+// overflowed shard with topk_f64_materialised.
 int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double *dc, int64_t ldc, int64_t n,
                          int64_t d, int64_t k, int metric, uint32_t index_base, uint32_t *oi, double *os, char *w,
-                         hipStream_t s, bool fused, const double *cn_pre = nullptr) {
+                         hipStream_t s, bool fused, const double *cn_pre = nullptr, unsigned *flag_copy = nullptr) {
   if (!fused)
     return topk_f64_materialised(dq, ldq, m, dc, ldc, n, d, k, metric, index_base, oi, os, w, s, cn_pre);
   F64Plan p;
@@ -1640,12 +1644,227 @@ int topk_f64_device_impl(const double *dq, int64_t ldq, int64_t m, const double 
       chunk = seen * g;
     }
   }
+  if (flag_copy) {
+    HIP_TRY(hipMemcpyAsync(flag_copy, flag, 4, hipMemcpyDeviceToDevice, s));
+    return PMM_OK;
+  }
   // an overflowed row dropped candidates: redo the call on the materialised path
   unsigned of = 0;
   HIP_TRY(hipMemcpyAsync(&of, flag, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   if (of) return topk_f64_materialised(dq, ldq, m, dc, ldc, n, d, k, metric, index_base, oi, os, w, s, cn_pre);
   return PMM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Corpus-sharded f64 top-k (the drop-in path of Polars' default Float64
+// columns under pmm_set_devices): the f32 path's plan (topk_sharded) with the
+// f64 top-k per shard.  Every device gets the queries once; each shard runs
+// topk_f64_device_impl on its rows with index_base = its first global row,
+// k_g = min(k, rows) (a shorter list is padded with empty slots); the fused
+// scans' overflow flags are read only after every device has finished (an
+// overflowed shard re-runs materialised, as one device would); the [m][k]
+// lists meet in the root's [G][m][k] planes by peer copies and
+// f64_kway_merge_kernel merges them.  A shard's list is the exact top-k of
+// its rows under the f64 total order, so the merged list equals the
+// one-device result bit for bit (indices and f64 scores).
+// ---------------------------------------------------------------------------
+struct ShardSrc64 {
+  int dev;
+  int64_t lo, rows;
+  const double *host;       // host rows [lo, lo + rows), row stride d, or
+  const double *dev_rows;   // a corpus handle's resident padded rows (stride dp)
+  const double *dev_norms;  // with dev_rows: the handle's norms of this metric (nullptr for dot)
+};
+
+int topk_sharded_f64(const double *q, int64_t m, int64_t d, int64_t k, int metric, const std::vector<ShardSrc64> &sh,
+                     uint32_t *out_idx, double *out_score) {
+  const int G = (int)sh.size();
+  int cur = 0;
+  HIP_TRY(hipGetDevice(&cur));
+  struct Restore {
+    int d;
+    ~Restore() { (void)hipSetDevice(d); }
+  } restore{cur};
+  const int64_t dp = cdiv(d, 16) * 16;
+  const int root = sh[0].dev;
+  for (const ShardSrc64 &x : sh)
+    if (int rc = probe_device(x.dev)) return rc;
+  struct Dev64 {
+    int dev;
+    hipStream_t s = nullptr;
+    char *base = nullptr;
+    size_t off_q = 0, off_ws = 0, ws_bytes = 0, off_flags = 0, total = 0;
+  };
+  std::vector<Dev64> dps;
+  std::vector<int> plan_of(G), slot(G);
+  std::vector<int64_t> kg(G);
+  std::vector<bool> fused(G);
+  std::vector<size_t> off_c(G), off_tmp(G), off_li(G), off_ls(G);
+  for (int g = 0; g < G; g++) {
+    int j = 0;
+    while (j < (int)dps.size() && dps[j].dev != sh[g].dev) j++;
+    if (j == (int)dps.size()) dps.push_back(Dev64{sh[g].dev});
+    plan_of[g] = j;
+    kg[g] = std::min<int64_t>(k, sh[g].rows);
+    fused[g] = f64_use_fused(m, sh[g].rows, kg[g]);
+  }
+  for (int j = 0; j < (int)dps.size(); j++) {
+    Dev64 &p = dps[j];
+    size_t off = 0;
+    p.off_q = off;
+    off = al256(off + (size_t)m * dp * 8);
+    int ns = 0;
+    for (int g = 0; g < G; g++) {
+      if (plan_of[g] != j) continue;
+      slot[g] = ns++;
+      p.ws_bytes = std::max(p.ws_bytes, f64_workspace_bytes(m, sh[g].rows, kg[g], fused[g]));
+      off_c[g] = off;
+      if (sh[g].host) off = al256(off + (size_t)sh[g].rows * dp * 8);
+      off_tmp[g] = off;
+      if (kg[g] < k) off = al256(off + (size_t)m * kg[g] * 12);
+      off_li[g] = off;
+      off = al256(off + (size_t)m * k * 4);
+      off_ls[g] = off;
+      off = al256(off + (size_t)m * k * 8);
+    }
+    p.off_flags = off;
+    off = al256(off + (size_t)ns * 4);
+    p.off_ws = off;
+    off = al256(off + p.ws_bytes);
+    p.total = off;
+  }
+  Dev64 &rp = dps[plan_of[0]];
+  const size_t off_gi = rp.total, off_gs = al256(off_gi + (size_t)G * m * k * 4);
+  const size_t off_oi = al256(off_gs + (size_t)G * m * k * 8), off_os = al256(off_oi + (size_t)m * k * 4);
+  rp.total = al256(off_os + (size_t)m * k * 8);
+  for (auto &p : dps) {
+    HIP_TRY(hipSetDevice(p.dev));
+    if (int rc = thread_stream(p.dev, &p.s)) return rc;
+    void *b;
+    if (int rc = arena(p.dev, p.s, p.total, &b)) return rc;
+    p.base = (char *)b;
+  }
+  std::vector<hipEvent_t> ev(G, nullptr);
+  auto finish = [&](int code) {
+    if (code != PMM_OK)
+      for (auto &p : dps) {
+        (void)hipSetDevice(p.dev);
+        (void)hipStreamSynchronize(p.s);
+      }
+    for (int g = 0; g < G; g++)
+      if (ev[g]) {
+        (void)hipSetDevice(sh[g].dev);
+        (void)hipEventDestroy(ev[g]);
+      }
+    return code;
+  };
+#define SH_TRY(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return finish(fail(PMM_ERR_HIP, "HIP error %s at %s:%d (%s)", hipGetErrorString(e_), \
+                         __FILE__, __LINE__, #expr));                                     \
+  } while (0)
+#define SH_RC(expr)                        \
+  do {                                     \
+    int rc_ = (expr);                      \
+    if (rc_ != PMM_OK) return finish(rc_); \
+  } while (0)
+  for (auto &p : dps) {
+    SH_TRY(hipSetDevice(p.dev));
+    SH_RC(upload_padded(p.base + p.off_q, q, m, d, dp, 8, p.s));
+  }
+  // per shard: rows, f64 top-k with global indices (every device at once:
+  // the overflow flags are copied, not waited for)
+  auto run_shard = [&](int g, bool materialised) -> int {
+    Dev64 &p = dps[plan_of[g]];
+    const ShardSrc64 &x = sh[g];
+    const double *c = x.dev_rows;
+    if (x.host) c = (const double *)(p.base + off_c[g]);
+    uint32_t *li = (uint32_t *)(p.base + off_li[g]);
+    double *ls = (double *)(p.base + off_ls[g]);
+    uint32_t *oi = li;
+    double *os = ls;
+    if (kg[g] < k) {
+      // a shard shorter than k: its kg best into a compact list, then into
+      // the [m][k] rows behind empty slots (idx 0xFFFFFFFF, score NaN)
+      oi = (uint32_t *)(p.base + off_tmp[g]);
+      os = (double *)(oi + (size_t)m * kg[g]);
+      HIP_TRY(hipMemsetAsync(li, 0xFF, (size_t)m * k * 4, p.s));
+      HIP_TRY(hipMemsetAsync(ls, 0xFF, (size_t)m * k * 8, p.s));  // (all-ones f64: a NaN)
+    }
+    unsigned *flag = (unsigned *)(p.base + p.off_flags) + slot[g];
+    int rc = materialised ? topk_f64_materialised((const double *)(p.base + p.off_q), dp, m, c, dp, x.rows, d,
+                                                  kg[g], metric, (uint32_t)x.lo, oi, os, p.base + p.off_ws, p.s,
+                                                  x.dev_norms)
+                          : topk_f64_device_impl((const double *)(p.base + p.off_q), dp, m, c, dp, x.rows, d, kg[g],
+                                                 metric, (uint32_t)x.lo, oi, os, p.base + p.off_ws, p.s, fused[g],
+                                                 x.dev_norms, fused[g] ? flag : nullptr);
+    if (rc) return rc;
+    if (kg[g] < k) {
+      HIP_TRY(hipMemcpy2DAsync(li, (size_t)k * 4, oi, (size_t)kg[g] * 4, (size_t)kg[g] * 4, (size_t)m,
+                               hipMemcpyDeviceToDevice, p.s));
+      HIP_TRY(hipMemcpy2DAsync(ls, (size_t)k * 8, os, (size_t)kg[g] * 8, (size_t)kg[g] * 8, (size_t)m,
+                               hipMemcpyDeviceToDevice, p.s));
+    }
+    return PMM_OK;
+  };
+  for (int g = 0; g < G; g++) {
+    Dev64 &p = dps[plan_of[g]];
+    SH_TRY(hipSetDevice(p.dev));
+    if (sh[g].host) SH_RC(upload_padded(p.base + off_c[g], sh[g].host, sh[g].rows, d, dp, 8, p.s));
+    SH_TRY(hipMemsetAsync((unsigned *)(p.base + p.off_flags) + slot[g], 0, 4, p.s));
+    SH_RC(run_shard(g, false));
+  }
+  // overflow flags, once every device is done: an overflowed shard re-runs
+  // on the materialised path (its rows, its workspace)
+  for (auto &p : dps) {
+    SH_TRY(hipSetDevice(p.dev));
+    SH_TRY(hipStreamSynchronize(p.s));
+  }
+  for (int g = 0; g < G; g++) {
+    Dev64 &p = dps[plan_of[g]];
+    SH_TRY(hipSetDevice(p.dev));
+    if (fused[g]) {
+      unsigned of = 0;
+      SH_TRY(hipMemcpy(&of, (unsigned *)(p.base + p.off_flags) + slot[g], 4, hipMemcpyDeviceToHost));
+      if (of) SH_RC(run_shard(g, true));
+    }
+    SH_TRY(hipEventCreateWithFlags(&ev[g], hipEventDisableTiming));
+    SH_TRY(hipEventRecord(ev[g], p.s));
+  }
+  // gather into the root (peer copies over xGMI), merge, download
+  SH_TRY(hipSetDevice(root));
+  uint32_t *gi = (uint32_t *)(rp.base + off_gi);
+  double *gs = (double *)(rp.base + off_gs);
+  for (int g = 0; g < G; g++) {
+    enable_peer(root, sh[g].dev);
+    SH_TRY(hipStreamWaitEvent(rp.s, ev[g], 0));
+    const char *pb = dps[plan_of[g]].base;
+    SH_TRY(hipMemcpyPeerAsync(gi + (size_t)g * m * k, root, pb + off_li[g], sh[g].dev, (size_t)m * k * 4, rp.s));
+    SH_TRY(hipMemcpyPeerAsync(gs + (size_t)g * m * k, root, pb + off_ls[g], sh[g].dev, (size_t)m * k * 8, rp.s));
+  }
+  F64MergeArgs ma{};
+  ma.gi = gi;
+  ma.gs = gs;
+  ma.list_stride = m * k;
+  ma.M = (int)m;
+  ma.G = G;
+  ma.k = (int)k;
+  ma.metric = metric;
+  ma.out_idx = (uint32_t *)(rp.base + off_oi);
+  ma.out_score = (double *)(rp.base + off_os);
+  {
+    Timed t("merge_devices_f64", rp.s);
+    SH_TRY(launch_f64_merge(ma, rp.s));
+  }
+  SH_TRY(hipMemcpyAsync(out_idx, ma.out_idx, (size_t)m * k * 4, hipMemcpyDeviceToHost, rp.s));
+  SH_TRY(hipMemcpyAsync(out_score, ma.out_score, (size_t)m * k * 8, hipMemcpyDeviceToHost, rp.s));
+  SH_TRY(hipStreamSynchronize(rp.s));
+#undef SH_TRY
+#undef SH_RC
+  return finish(PMM_OK);
 }
 
 std::vector<int> devices_snapshot() {
@@ -1656,7 +1875,7 @@ std::vector<int> devices_snapshot() {
 // The device host entry points run on when a device list is set: its first
 // entry (the root, which also merges a sharded search), else -1 (the thread's
 // pmm_set_device choice or the current device).  A one-entry list therefore
-// moves all host work to that device; work that is not sharded (f64, k > 1024,
+// moves all host work to that device; work that is not sharded (f32 k > 1024,
 // .pmm.matmul) runs on the root of a longer list.
 int list_root() {
   std::lock_guard<std::mutex> lk(g_devs_mu);
@@ -1674,8 +1893,8 @@ int64_t shard_lo(int64_t n, int G, int g) { return n * g / G; }
 // devices at creation, one contiguous shard each.
 // A Float64 corpus (pmm_corpus_create_f64; Polars' default float columns
 // take the reference's f64 branch, src/matmul.rs:449-468) keeps its rows in
-// f64 on one device with the f64 norms of both metrics; f64 work is not
-// sharded.
+// f64 with the f64 norms of both metrics, sharded over a device list the same
+// way (round 6).
 struct CorpusShard {
   int device = 0;
   int64_t lo = 0, n = 0;       // rows [lo, lo + n) of the corpus
@@ -2009,6 +2228,20 @@ int pmm_topk_f64(const double *q, int64_t m, const double *c, int64_t n, int64_t
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
   if ((rc = need_buffers(q, c, out_idx, out_score))) return rc;
+  {
+    // a device list (pmm_set_devices): the corpus row-sharded over it, as the
+    // f32 path does (topk_sharded_f64)
+    const std::vector<int> devs = devices_snapshot();
+    if (devs.size() > 1 && n > 1) {
+      const int G = (int)std::min<int64_t>((int64_t)devs.size(), n);
+      std::vector<ShardSrc64> sh(G);
+      for (int g = 0; g < G; g++) {
+        const int64_t lo = shard_lo(n, G, g), hi = shard_lo(n, G, g + 1);
+        sh[g] = ShardSrc64{devs[g], lo, hi - lo, c + lo * d, nullptr, nullptr};
+      }
+      return topk_sharded_f64(q, m, d, k, metric, sh, out_idx, out_score);
+    }
+  }
   int dev;
   DevScope scope;
   if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
@@ -2318,38 +2551,53 @@ int pmm_corpus_create_f64(const double *c, int64_t n, int64_t d, pmm_corpus **ou
   if (!c) return fail(PMM_ERR_ARG, "null argument");
   int dev;
   DevScope scope;
-  if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;  // f64 is not sharded: the list's root
-  hipStream_t s;
-  if ((rc = thread_stream(dev, &s))) return rc;
+  if ((rc = ensure_device(&dev, &scope, list_root()))) return rc;
+  // with a device list the rows are sharded over it, as pmm_corpus_create_f32
+  // does (one contiguous shard per listed device, at most n)
+  std::vector<int> devs = devices_snapshot();
+  if (devs.size() <= 1) devs.assign(1, dev);
+  const int G = (int)std::min<int64_t>((int64_t)devs.size(), n);
   pmm_corpus *h = new pmm_corpus();
   h->n = n;
   h->d = d;
   h->dp = cdiv(d, 16) * 16;  // the f64 kernels' K step (pmm_topk_f64_device's stride rule)
   h->dtype = PMM_DTYPE_F64;
-  h->shards.resize(1);
-  CorpusShard &x = h->shards[0];
-  x.device = dev;
-  x.lo = 0;
-  x.n = n;
-  hipError_t e = hipMalloc(&x.data64, (size_t)n * h->dp * 8);
-  if (e == hipSuccess) e = hipMalloc(&x.norms64, (size_t)n * 2 * 8);
-  if (e != hipSuccess) {
-    pmm_corpus_destroy(h);
-    return fail(PMM_ERR_HIP, "corpus allocation failed on device %d: %s", dev, hipGetErrorString(e));
+  h->shards.resize(G);
+  for (int g = 0; g < G; g++) {
+    CorpusShard &x = h->shards[g];
+    x.device = devs[g];
+    x.lo = shard_lo(n, G, g);
+    x.n = shard_lo(n, G, g + 1) - x.lo;
   }
-  if ((rc = upload_padded(x.data64, c, n, d, h->dp, 8, s))) {
-    pmm_corpus_destroy(h);
-    return rc;
+  for (int g = 0; g < G; g++) {
+    CorpusShard &x = h->shards[g];
+    hipStream_t s;
+    hipError_t e = hipSetDevice(x.device);
+    if (e == hipSuccess && (rc = thread_stream(x.device, &s))) {
+      pmm_corpus_destroy(h);
+      return rc;
+    }
+    if (e == hipSuccess) e = hipMalloc(&x.data64, (size_t)x.n * h->dp * 8);
+    if (e == hipSuccess) e = hipMalloc(&x.norms64, (size_t)x.n * 2 * 8);
+    if (e != hipSuccess) {
+      pmm_corpus_destroy(h);
+      return fail(PMM_ERR_HIP, "corpus allocation failed on device %d: %s", x.device, hipGetErrorString(e));
+    }
+    if ((rc = upload_padded(x.data64, c + x.lo * d, x.n, d, h->dp, 8, s))) {
+      pmm_corpus_destroy(h);
+      return rc;
+    }
+    // the norms every f64 call would compute (src/metrics.rs:368-379), by the
+    // same kernel on the same padded rows: bit-identical to the per-call ones
+    hipError_t e1 = launch_norms_f64(x.data64, x.n, d, h->dp, 0, x.norms64, s);
+    hipError_t e2 = launch_norms_f64(x.data64, x.n, d, h->dp, 1, x.norms64 + x.n, s);
+    hipError_t e3 = hipStreamSynchronize(s);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
+      pmm_corpus_destroy(h);
+      return fail(PMM_ERR_HIP, "corpus norms failed");
+    }
   }
-  // the norms every f64 call would compute (src/metrics.rs:368-379), by the
-  // same kernel on the same padded rows: bit-identical to the per-call ones
-  hipError_t e1 = launch_norms_f64(x.data64, n, d, h->dp, 0, x.norms64, s);
-  hipError_t e2 = launch_norms_f64(x.data64, n, d, h->dp, 1, x.norms64 + n, s);
-  hipError_t e3 = hipStreamSynchronize(s);
-  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) {
-    pmm_corpus_destroy(h);
-    return fail(PMM_ERR_HIP, "corpus norms failed");
-  }
+  (void)hipSetDevice(dev);
   *out = h;
   return PMM_OK;
 }
@@ -2364,6 +2612,15 @@ int pmm_topk_f64_corpus(const pmm_corpus *h, const double *q, int64_t m, int64_t
   if ((rc = check_metric(metric))) return rc;
   if (m == 0 || k == 0) return PMM_OK;
   if ((rc = need_buffers(q, out_idx, out_score))) return rc;
+  if (h->shards.size() > 1) {
+    std::vector<ShardSrc64> sh(h->shards.size());
+    for (size_t g = 0; g < sh.size(); g++) {
+      const CorpusShard &x = h->shards[g];
+      const double *cn = metric == kMetricCosine ? x.norms64 : metric == kMetricEuclidean ? x.norms64 + x.n : nullptr;
+      sh[g] = ShardSrc64{x.device, x.lo, x.n, nullptr, x.data64, cn};
+    }
+    return topk_sharded_f64(q, m, h->d, k, metric, sh, out_idx, out_score);
+  }
   const CorpusShard &x = h->shards[0];
   int dev;
   DevScope scope;

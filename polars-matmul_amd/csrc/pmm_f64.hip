@@ -266,7 +266,10 @@ __global__ __launch_bounds__(256, W == 4 ? 2 : 1) void gemm_f64_topk_kernel(F64T
   for (int tj = 0; tj < W; tj++) {
     const int lc = lc0 + 16 * tj + i;
     const double cvv = (METRIC == kMetricCosine && lc < a.ncol) ? a.cn[a.col0 + lc] : 0.0;
-    cnf[tj] = cvv > 1e-10 ? cvv : kNaN;
+    // (a column factor in [1e-10, 2^100] and a row bound |bm| in [2^-900,
+    // 2^900] keep bm * cn a normal double, where the rounding margin below
+    // holds; outside, NaN: no skip, the exact division decides)
+    cnf[tj] = (cvv > 1e-10 && cvv < 0x1p100) ? cvv : kNaN;
   }
 #pragma unroll
   for (int ti = 0; ti < W; ti++) {
@@ -282,8 +285,9 @@ __global__ __launch_bounds__(256, W == 4 ? 2 : 1) void gemm_f64_topk_kernel(F64T
       double bm = kNaN;
       if (METRIC == kMetricCosine) {
         const double ts = dekey64(tk);
-        if (qv > 1e-10 && ts != 0.0)
-          bm = __dmul_rn(__dmul_rn(ts, qv), ts > 0.0 ? 1.0 - 0x1p-49 : 1.0 + 0x1p-49);
+        const double tq = __dmul_rn(ts, qv);
+        if (qv > 1e-10 && ts != 0.0 && fabs(tq) > 0x1p-900 && fabs(tq) < 0x1p900)
+          bm = __dmul_rn(tq, ts > 0.0 ? 1.0 - 0x1p-49 : 1.0 + 0x1p-49);
       }
 #pragma unroll
       for (int tj = 0; tj < W; tj++) {
@@ -495,6 +499,86 @@ __global__ __launch_bounds__(256) void f64_reset_kernel(u64 *tkey, uint32_t *tid
     tidx[r] = 0xFFFFFFFFu;
     cnt[r] = cnt0;
   }
+}
+
+// ---------------------------------------------------------------------------
+// k-way merge of G sorted f64 lists per row (the corpus-sharded f64 path:
+// every device's f64 top-k of its shard, gathered into [G][m][k] index and
+// score planes on the root).  LPR = next_pow2(G) lanes per row, lane g holding
+// list g's head; per output position the row's best head under the f64
+// path's total order (key okey64(score) best-first -- NaN and empty slots at
+// key 0 -- then the lower index; empty slots carry 0xFFFFFFFF, so they come
+// last) by log2(LPR) shuffle steps, and the winning list advances.  The
+// winner writes the entry as its list holds it (bit for bit the one-device
+// value).  Each list's next entry is loaded ahead of its next win.
+// ---------------------------------------------------------------------------
+template <int LPR>
+__global__ __launch_bounds__(256) void f64_kway_merge_kernel(F64MergeArgs a) {
+  const int lane = threadIdx.x & 63;
+  constexpr int RPW = 64 / LPR;
+  const int wave = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int row = wave * RPW + lane / LPR;
+  const int g = lane % LPR;
+  if (wave * RPW >= a.M) return;  // whole wave exits
+  const bool live = row < a.M && g < a.G;
+  const int64_t base = live ? (int64_t)g * a.list_stride + (int64_t)row * a.k : 0;
+  const double nan = __longlong_as_double(0x7FF8000000000000ll);
+  auto ld = [&](int p, uint32_t &id, double &sc) __attribute__((always_inline)) {
+    const bool ok = live && p < a.k;
+    const int64_t o = ok ? base + p : 0;
+    id = a.gi[o];
+    sc = a.gs[o];
+    if (!ok) id = 0xFFFFFFFFu;
+  };
+  uint32_t hid, nid;
+  double hsc, nsc;
+  ld(0, hid, hsc);
+  ld(1, nid, nsc);
+  int ptr = 0;
+  for (int j = 0; j < a.k; j++) {
+    const u64 hk = hid != 0xFFFFFFFFu ? f64_key(hsc, a.metric) : 0ull;
+    u64 mk = hk;
+    uint32_t mi = hid;
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) {
+      const u64 ok2 = __shfl_xor(mk, o);
+      const uint32_t oi2 = (uint32_t)__shfl_xor((int)mi, o);
+      if (ok2 > mk || (ok2 == mk && oi2 < mi)) {
+        mk = ok2;
+        mi = oi2;
+      }
+    }
+    // the lists' (key, index) pairs are distinct (disjoint shard rows), so
+    // one lane wins -- or, past every list's end, all lanes hold the same
+    // empty slot and write the same empty entry
+    if (live && hk == mk && hid == mi) {
+      a.out_idx[(int64_t)row * a.k + j] = hid;
+      a.out_score[(int64_t)row * a.k + j] = hid != 0xFFFFFFFFu ? hsc : nan;
+      ptr++;
+      hid = nid;
+      hsc = nsc;
+      ld(ptr + 1, nid, nsc);
+    }
+  }
+}
+
+hipError_t launch_f64_merge(const F64MergeArgs &a, hipStream_t s) {
+  if (a.M <= 0 || a.k <= 0) return hipSuccess;
+  int lpr = 1;
+  while (lpr < a.G) lpr <<= 1;
+  if (lpr > 64) return hipErrorInvalidValue;
+  const int64_t waves = ((int64_t)a.M * lpr + 63) / 64;
+  const unsigned grid = (unsigned)((waves + 3) / 4);
+  switch (lpr) {
+    case 1: f64_kway_merge_kernel<1><<<grid, 256, 0, s>>>(a); break;
+    case 2: f64_kway_merge_kernel<2><<<grid, 256, 0, s>>>(a); break;
+    case 4: f64_kway_merge_kernel<4><<<grid, 256, 0, s>>>(a); break;
+    case 8: f64_kway_merge_kernel<8><<<grid, 256, 0, s>>>(a); break;
+    case 16: f64_kway_merge_kernel<16><<<grid, 256, 0, s>>>(a); break;
+    case 32: f64_kway_merge_kernel<32><<<grid, 256, 0, s>>>(a); break;
+    default: f64_kway_merge_kernel<64><<<grid, 256, 0, s>>>(a); break;
+  }
+  return hipGetLastError();
 }
 
 hipError_t launch_f64_reset(u64 *tkey, uint32_t *tidx, unsigned *cnt, int m, unsigned cnt0, hipStream_t s) {

@@ -217,6 +217,17 @@ struct F64SelArgs {
   double *out_score;
   unsigned *overflow;        // set when a row's count exceeded cap (entries were dropped)
 };
+// k-way merge of G (<= 64) sorted f64 top-k lists per row: entry i of list g
+// of row r at gi / gs[g * list_stride + r * k + i]
+struct F64MergeArgs {
+  const uint32_t *gi;
+  const double *gs;
+  int64_t list_stride;
+  int M, G, k, metric;
+  uint32_t *out_idx;    // [M][k]
+  double *out_score;
+};
+hipError_t launch_f64_merge(const F64MergeArgs &a, hipStream_t s);
 hipError_t launch_gemm_f64_topk(const F64TopkArgs &a, hipStream_t s);
 hipError_t launch_f64_select(const F64SelArgs &a, hipStream_t s);
 hipError_t launch_f64_reset(unsigned long long *tkey, uint32_t *tidx, unsigned *cnt, int m, unsigned cnt0,

@@ -316,7 +316,6 @@ class PinnedPool:
         self.idle = 0
         self.lock = threading.Lock()
         self.returned = collections.deque()  # (ptr, nbytes) from finalisers, lock-free
-        self.pending = 0  # bytes waiting in `returned` (approximate: updated without the lock)
 
     def _absorb(self):
         """Move finalised blocks into the free lists (lock held by caller).
@@ -328,7 +327,6 @@ class PinnedPool:
                 p, nbytes = self.returned.popleft()
             except IndexError:
                 return over
-            self.pending -= nbytes
             if self.idle + nbytes <= self.cap:
                 self.free.setdefault(nbytes, []).append(p)
                 self.idle += nbytes
@@ -360,11 +358,13 @@ class PinnedPool:
         # runs from finalisers: never waits on the lock (the finaliser may run
         # inside `take` on the thread that holds it), allocates nothing beyond
         # the deque node before it tries the lock
-        self.pending += nbytes
         self.returned.append((p, nbytes))
         # opportunistic drain: blocks past the cap are freed as they come back,
         # not left page-locked until a later take(); when the lock
-        # is busy, its holder or the next call drains them
+        # is busy, its holder or the next call drains them.  Not at interpreter
+        # shutdown (module globals may be gone; the process exit frees them)
+        if sys.is_finalizing() or _lib is None:
+            return
         self.drain(blocking=False)
 
     def drain(self, blocking: bool = True) -> None:
@@ -379,7 +379,9 @@ class PinnedPool:
             _lib.pmm_host_free(q)
 
     def pending_bytes(self) -> int:
-        return max(0, self.pending)
+        """Bytes returned by finalisers and not yet absorbed (from the deque
+        itself, so no unlocked counter can drift)."""
+        return sum(n for _, n in list(self.returned))
 
     def idle_bytes(self) -> int:
         with self.lock:

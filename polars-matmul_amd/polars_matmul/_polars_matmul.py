@@ -371,8 +371,8 @@ def _topk(left, right, k, metric):
     else:
         _apply_devices_env()
         # (an f32 handle sharded over several GPUs serves k <= 1024; larger k
-        # runs on one GPU, the device list's first.  An f64 handle lives on
-        # one GPU and serves any k.)
+        # runs on one GPU, the device list's first.  An f64 handle is sharded
+        # the same way and serves any k.)
         dc = (_cached_corpus(right, rv, c)
               if (not use_f32 or kk <= 1024 or len(_native.get_devices()) <= 1) else None)
         if dc is not None:

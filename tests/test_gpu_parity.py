@@ -252,6 +252,31 @@ def test_f64_cosine_division_skip_at_threshold_edges(pmm, k, monkeypatch):
     assert np.array_equal(mi, idx) and np.array_equal(ms.view(np.uint64), sc.view(np.uint64))
 
 
+def test_f64_cosine_division_skip_tiny_scores(pmm, monkeypatch):
+    # cosine scores around 1e-300 (products near the subnormal
+    # range, where the skip's rounding margin would not hold) and thresholds
+    # on exact ties among them: the skip must stand aside there -- fused ==
+    # oracle == materialised, bit for bit
+    monkeypatch.setenv("PMM_F64_FUSED", "1")
+    rs = np.random.RandomState(3)
+    n, d, k = 4000, 4, 50
+    q = np.zeros((4, d))
+    q[:, 0] = 1.0
+    q[:, 1] = [1e-300, 3e-301, 1e-305, 2.5e-290]
+    c = np.zeros((n, d))
+    c[:, 1] = rs.randint(-40, 41, size=n) * 1.0   # many exact ties
+    c[:, 2] = 1.0                                  # corpus norms ~ |c[:, 1]|
+    c[::7, 1] = rs.randn(len(c[::7])) * 1e-3
+    idx, sc = gpu_topk(q, c, k, "cosine")
+    oi, osc = oracle.topk(q, c, k, METRICS["cosine"])
+    assert np.array_equal(idx, oi)
+    assert np.array_equal(sc.view(np.uint64), osc.view(np.uint64))
+    assert np.all(np.abs(sc[np.isfinite(sc)]) < 1e-280)
+    monkeypatch.setenv("PMM_F64_FUSED", "0")
+    mi, ms = gpu_topk(q, c, k, "cosine")
+    assert np.array_equal(mi, idx) and np.array_equal(ms.view(np.uint64), sc.view(np.uint64))
+
+
 def test_f64_fused_overflow_falls_back(pmm, monkeypatch):
     # adversarial order: every corpus row beats every earlier one, so each
     # chunk's survivors overflow the buffers; the call must still be exact
@@ -1409,6 +1434,77 @@ def test_set_devices_one_entry_runs_there(pmm, device_list):
     dc.close()
 
 
+@pytest.mark.parametrize("shards", [2, 3, 8])
+@pytest.mark.parametrize("metric", ["cosine", "dot", "euclidean"])
+def test_set_devices_sharded_f64_bitexact(pmm, device_list, shards, metric, monkeypatch):
+    # the f64 branch (Polars' default Float64 columns,
+    # src/matmul.rs:449-468) sharded under a device list: every shard's f64
+    # top-k with global indices, merged on the root -- bit-equal to one
+    # device (indices and f64 scores), on both f64 paths, with ties across
+    # shard boundaries, through the host API and a sharded f64 corpus handle
+    n = device_list
+    rs = np.random.RandomState(shards * 11 + len(metric))
+    m, N, d, k = 120, 9001, 64, 100
+    q = rs.randn(m, d)
+    c = rs.randn(N, d)
+    c[N - 30:] = c[:30]  # exact ties across shard boundaries
+    for fused in ("1", "0"):
+        monkeypatch.setenv("PMM_F64_FUSED", fused)
+        n.set_devices([])
+        want = n.topk_host(q, c, k, METRICS[metric])
+        one = n.DeviceCorpus(c)
+        n.set_devices([0] * shards)
+        got = n.topk_host(q, c, k, METRICS[metric])
+        assert np.array_equal(got[0], want[0]), (fused, float(np.mean(got[0] == want[0])))
+        assert np.array_equal(got[1].view(np.uint64), want[1].view(np.uint64)), fused
+        dc = n.DeviceCorpus(c)
+        assert dc.shards == shards and one.shards == 1
+        gc = dc.topk(q, k, METRICS[metric])
+        assert np.array_equal(gc[0], want[0]) and np.array_equal(gc[1].view(np.uint64), want[1].view(np.uint64))
+        oc = one.topk(q, k, METRICS[metric])
+        assert np.array_equal(oc[0], want[0])
+        dc.close()
+        one.close()
+    oi, osc = oracle.topk(q, c, k, METRICS[metric])
+    assert np.array_equal(got[0], oi) and np.array_equal(got[1].view(np.uint64), osc.view(np.uint64))
+
+
+def test_set_devices_f64_shards_smaller_than_k_and_large_k(pmm, device_list):
+    # shards shorter than k (their lists padded with empty slots) and k above
+    # the fused limit (every shard materialised): still the one-device lists
+    n = device_list
+    rs = np.random.RandomState(17)
+    q = rs.randn(30, 40)
+    c = rs.randn(101, 40)
+    want = n.topk_host(q, c, 64, METRICS["cosine"])
+    n.set_devices([0] * 8)  # 8 shards of 12-13 rows, k = 64
+    got = n.topk_host(q, c, 64, METRICS["cosine"])
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1].view(np.uint64), want[1].view(np.uint64))
+    n.set_devices([])
+    c2 = rs.randn(6000, 40)
+    want = n.topk_host(q, c2, 1500, METRICS["dot"])
+    n.set_devices([0, 0, 0])
+    got = n.topk_host(q, c2, 1500, METRICS["dot"])
+    assert np.array_equal(got[0], want[0]) and np.array_equal(got[1].view(np.uint64), want[1].view(np.uint64))
+
+
+def test_set_devices_f64_through_extension_and_cache(pmm, device_list):
+    from polars_matmul import _polars_matmul as pm
+
+    rs = np.random.RandomState(8)
+    q = rs.randn(40, 96)
+    c = rs.randn(7000, 96)
+    carr = pa.FixedSizeListArray.from_arrays(pa.array(c.reshape(-1)), 96)
+    qarr = pa.FixedSizeListArray.from_arrays(pa.array(q.reshape(-1)), 96)
+    want = pm._topk(qarr, carr, 25, "euclidean").to_pylist()
+    pm.set_devices([0, 0, 0])
+    try:
+        for _ in range(2):  # second call: the sharded cached f64 handle
+            assert pm._topk(qarr, carr, 25, "euclidean").to_pylist() == want
+    finally:
+        pm.clear_corpus_cache()
+
+
 def _visible_gpus():
     try:
         return _native().device_count()
@@ -1444,6 +1540,13 @@ def test_set_devices_distinct_gpus(pmm, device_list, metric):
     n.set_devices(list(reversed(range(G))))  # root on the last device
     got = n.topk_host(q, c, 100, METRICS[metric])
     assert np.array_equal(got[0], want[0])
+    # the f64 branch over the same distinct devices
+    q64, c64 = q[:100].astype(np.float64), c[:20000].astype(np.float64)
+    n.set_devices([])
+    want64 = n.topk_host(q64, c64, 100, METRICS[metric])
+    n.set_devices(list(range(G)))
+    got64 = n.topk_host(q64, c64, 100, METRICS[metric])
+    assert np.array_equal(got64[0], want64[0]) and np.array_equal(got64[1].view(np.uint64), want64[1].view(np.uint64))
 
 
 # ---- the fire-and-forget 256-row bf16 kernel (pmm_bf16_ff_kernel.h,

@@ -137,3 +137,44 @@ def test_f64_mfmas_keep_their_accumulators_in_vgprs():
     assert len(mfma) >= 6, sorted(mfma)  # store (3 metrics) + top-k (3 metrics x 2 tiles)
     bad = {f: c[1] for f, c in mfma.items() if c[1]}
     assert not bad, f"accumulator moves in f64 MFMA kernels: {bad}"
+
+
+def scratch_by_kernel(asm: str):
+    """{kernel: (private segment bytes, scratch instructions)} from the ISA's
+    kernel descriptors and bodies."""
+    sizes, counts, func, desc = {}, {}, None, None
+    for line in asm.splitlines():
+        m = re.match(r"^(_Z\S+):", line)
+        if m:
+            func = m.group(1)
+            counts.setdefault(func, 0)
+            continue
+        s = line.strip()
+        m = re.match(r"^\.amdhsa_kernel\s+(\S+)", s)
+        if m:
+            desc = m.group(1)
+            continue
+        m = re.match(r"^\.amdhsa_private_segment_fixed_size\s+(\d+)", s)
+        if m and desc:
+            sizes[desc] = int(m.group(1))
+            continue
+        if func and s.startswith("scratch_"):
+            counts[func] += 1
+    return {k: (sizes.get(k, -1), counts.get(k, 0)) for k in set(sizes) | set(counts)}
+
+
+@pytest.mark.skipif(not have_hipcc(), reason="hipcc not available")
+def test_f32_gemm_and_merge_kernels_use_no_scratch():
+    # ADVICE r5: the two-pass pre-filter reads acc[c][e] by a wave-uniform
+    # runtime index; that must stay a register-indexed move, never demote the
+    # accumulators to scratch (a compiler change could, silently).  And the
+    # merge kernels: a scratch-resident value read per candidate batch waits
+    # for every load in flight (scratch counts in vmcnt) -- round 5's
+    # threshold did, serialising the batch pipeline.
+    asm = all_isa()[("pmm_kernels.hip", ())]
+    sc = scratch_by_kernel(asm)
+    gemm = {k: v for k, v in sc.items() if "gemm_f32_kernel" in k}
+    merge = {k: v for k, v in sc.items() if "merge_kernel" in k}
+    assert len(gemm) >= 10 and len(merge) >= 5, (sorted(gemm)[:3], sorted(merge))
+    bad = {k: v for k, v in {**gemm, **merge}.items() if v != (0, 0)}
+    assert not bad, f"scratch (bytes, instructions) in: {bad}"
