@@ -46,8 +46,11 @@ extern "C" {
  * (v_mfma_f32_32x32x2_f32), the reference's precision.  BF16 = inputs rounded
  * to bf16 (round to nearest even) on device, products accumulated in f32
  * (v_mfma_f32_16x16x32_bf16), norms of the rounded rows in f32: the result is
- * the top-k of the bf16-rounded embeddings (BASELINE configs[3]); limits
- * d <= 768 and k <= 960 (PMM_ERR_UNSUPPORTED beyond). */
+ * the top-k of the bf16-rounded embeddings (BASELINE configs[3]).  The bf16
+ * MFMA kernels take d <= 768, k <= 960 and n < 2^27; beyond (configs[4]'s
+ * d = 1024, larger k) the rounded rows are widened to f32 exactly and
+ * searched by the f32 path: the same bar (exact top-k of the rounded rows up
+ * to f32 accumulation order) at the f32 MFMA rate. */
 #define PMM_COMPUTE_F32 0
 #define PMM_COMPUTE_BF16 1
 
@@ -216,8 +219,9 @@ int pmm_topk_f32_device(const float *q, int64_t ldq, int64_t m, const float *c, 
 /* The bf16 compute path over device-resident bf16 rows (bit patterns, e.g. a
  * torch.bfloat16 tensor): d is the logical dimension; ldq / ldc >=
  * roundup(d, 128), multiples of 8, columns past d zero-filled, 16-byte-aligned
- * bases; d <= 768, k <= 960.  Scores are f32 (see PMM_COMPUTE_BF16); k may
- * exceed n as in pmm_topk_f32_device. */
+ * bases (any d and k: past the bf16 kernels' limits, the widened f32 path of
+ * PMM_COMPUTE_BF16).  Scores are f32; k may exceed n as in
+ * pmm_topk_f32_device. */
 int pmm_topk_bf16_device(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c,
                          int64_t ldc, int64_t n, int64_t d, int64_t k, int metric,
                          uint32_t index_base, uint32_t *out_idx, float *out_score,

@@ -57,6 +57,24 @@ hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t
   return hipGetLastError();
 }
 
+// bf16 -> f32 (exact widening) with zero padding to ldd: one thread per element
+__global__ __launch_bounds__(256) void bf16_to_f32_kernel(const uint16_t *__restrict__ src, int64_t rows,
+                                                          int64_t d, int64_t lds, float *__restrict__ dst,
+                                                          int64_t ldd) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * ldd) return;
+  const int64_t r = t / ldd, c = t - r * ldd;
+  dst[t] = (c < d) ? __uint_as_float((uint32_t)src[r * lds + c] << 16) : 0.0f;
+}
+
+hipError_t launch_bf16_to_f32(const uint16_t *src, int64_t rows, int64_t d, int64_t lds, float *dst, int64_t ldd,
+                              hipStream_t s) {
+  if (rows <= 0) return hipSuccess;
+  const int64_t threads = rows * ldd;
+  bf16_to_f32_kernel<<<(unsigned)((threads + 255) / 256), 256, 0, s>>>(src, rows, d, lds, dst, ldd);
+  return hipGetLastError();
+}
+
 hipError_t launch_norms_bf16(const uint16_t *a, int64_t rows, int64_t d, int64_t ld, int squared,
                              float *out, float *inv, hipStream_t s) {
   if (rows <= 0) return hipSuccess;

@@ -817,17 +817,36 @@ int topk_f32_device_impl(const float *q, int64_t ldq, int64_t m, const float *c,
 
 // bf16 compute path over device bf16 rows (row strides ldq / ldc >=
 // roundup(d, 128), zero-padded); d is the logical dimension.
-int bf16_limits(int64_t d, int64_t k, int64_t n) {
-  if (cdiv(d, kBf16DAlign) * kBf16DAlign > kBf16MaxD)
-    return fail(PMM_ERR_UNSUPPORTED, "bf16 compute supports d <= %d (got %lld)", kBf16MaxD,
-                (long long)d);
-  if (n >= (int64_t(1) << 27))
-    return fail(PMM_ERR_UNSUPPORTED, "bf16 compute supports n < 2^27 corpus rows (got %lld)",
-                (long long)n);
-  if (next_pow2((int)std::min<int64_t>(k, 1 << 20) + 64, 128) > kBf16MaxCapg)
-    return fail(PMM_ERR_UNSUPPORTED, "bf16 compute supports k <= %d (got %lld)", kBf16MaxCapg - 64,
-                (long long)k);
-  return PMM_OK;
+//
+// The bf16 MFMA kernels hold a wave's 32 query rows x padded D in registers
+// (D <= 768), their candidate buffers take k <= 960 and pack the column into
+// 27 bits.  Outside that (configs[4]'s D = 1024, larger k, n >= 2^27) the
+// bf16 operands are widened to f32 -- exactly: a bf16 value is an f32 with
+// its low 16 bits zero -- and searched by the f32 path.  The result is the
+// exact top-k of the bf16-rounded rows with f32 products and a k-ordered f32
+// sum (the f32 path's bit-exact chain), so it meets the bf16 bar; the f32
+// MFMA runs at 1/16 of the bf16 rate, which the bench line of such a shape
+// states.
+bool bf16_native(int64_t d, int64_t k, int64_t n) {
+  return cdiv(d, kBf16DAlign) * kBf16DAlign <= kBf16MaxD && n < (int64_t(1) << 27) &&
+         next_pow2((int)std::min<int64_t>(k, 1 << 20) + 64, 128) <= kBf16MaxCapg;
+}
+
+size_t f32_topk_ws_bytes(int64_t m, int64_t n, int64_t dp, int64_t k, int metric, int cus) {
+  if (k <= kFusedMaxK) {
+    Plan p;
+    plan_topk(m, n, dp, k, metric, cus, p);
+    return p.total;
+  }
+  MatPlan p;
+  plan_materialise(m, n, k, 4, p);
+  return p.total;
+}
+
+// workspace of the widened path: the f32 rows, then the f32 search's own
+size_t bf16_widened_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus) {
+  const int64_t dp = cdiv(d, 32) * 32;
+  return al256((size_t)m * dp * 4) + al256((size_t)n * dp * 4) + f32_topk_ws_bytes(m, n, dp, k, metric, cus);
 }
 
 int ff_rerun(const uint16_t *q, int64_t ldq, int64_t m, const uint16_t *c, int64_t ldc, int64_t n, int64_t d,
@@ -839,6 +858,29 @@ int topk_bf16_device_impl(const uint16_t *q, int64_t ldq, int64_t m, const uint1
                           uint32_t index_base, uint32_t *out_idx, float *out_score, void *ws,
                           size_t ws_bytes, hipStream_t s, int dev) {
   const int cus = g_dev[dev].cus;
+  if (!bf16_native(d, k, n)) {
+    // widened to f32 and searched by the f32 path (see bf16_native)
+    const int64_t dp32 = cdiv(d, 32) * 32;
+    const size_t oc = al256((size_t)m * dp32 * 4), ow = oc + al256((size_t)n * dp32 * 4);
+    const size_t wsf = f32_topk_ws_bytes(m, n, dp32, k, metric, cus);
+    const bool own = !ws;
+    if (!ws) {
+      int rc = arena(dev, s, ow + wsf, &ws);
+      if (rc) return rc;
+    } else if (ws_bytes < ow + wsf) {
+      return fail(PMM_ERR_ARG, "workspace too small: %zu < %zu bytes", ws_bytes, ow + wsf);
+    }
+    char *w = (char *)ws;
+    {
+      Timed t("bf16_widen", s);
+      HIP_TRY(launch_bf16_to_f32(q, m, d, ldq, (float *)w, dp32, s));
+      HIP_TRY(launch_bf16_to_f32(c, n, d, ldc, (float *)(w + oc), dp32, s));
+    }
+    int rc = topk_f32_device_impl((const float *)w, dp32, m, (const float *)(w + oc), dp32, n, d, k, metric,
+                                  index_base, out_idx, out_score, w + ow, wsf, s, dev);
+    if (rc) return rc;
+    return own ? arena_record(dev, s) : PMM_OK;
+  }
   const int64_t dp = cdiv(d, kBf16DAlign) * kBf16DAlign;
   Plan p;
   plan_topk(m, n, dp, k, metric, cus, p, PMM_COMPUTE_BF16);
@@ -1288,9 +1330,15 @@ void plan_sharded(const std::vector<ShardSrc> &sh, int64_t m, int64_t d, int64_t
     off = al256(off + (bf16 ? (size_t)m * dp * 2 : 0));
     for (int g = 0; g < G; g++) {
       if (sh[g].dev != p.dev) continue;
-      Plan tp;
-      plan_topk(m, sh[g].rows, dp, k, metric, device_cus(p.dev), tp, compute);
-      p.ws_bytes = std::max(p.ws_bytes, tp.total);
+      size_t need;
+      if (bf16 && !bf16_native(d, k, sh[g].rows)) {
+        need = bf16_widened_bytes(m, sh[g].rows, d, k, metric, device_cus(p.dev));
+      } else {
+        Plan tp;
+        plan_topk(m, sh[g].rows, dp, k, metric, device_cus(p.dev), tp, compute);
+        need = tp.total;
+      }
+      p.ws_bytes = std::max(p.ws_bytes, need);
       L.off_c[g] = off;
       if (sh[g].host) off = al256(off + (size_t)sh[g].rows * (bf16 ? d : dp) * 4);
       L.off_cb[g] = off;
@@ -2030,6 +2078,7 @@ size_t pmm_topk_workspace_bytes(int64_t m, int64_t n, int64_t d, int64_t k, int 
     if (dev >= 0 && dev < kMaxDevices && g_dev[dev].probed) cus = g_dev[dev].cus;
   }
   if (compute == PMM_COMPUTE_BF16) {
+    if (!bf16_native(d, k, n)) return bf16_widened_bytes(m, n, d, k, metric, cus);
     Plan p;
     plan_topk(m, n, d, k, metric, cus, p, PMM_COMPUTE_BF16);
     return p.total;
@@ -2114,7 +2163,6 @@ int pmm_topk_f32_ex(const float *q, int64_t m, const float *c, int64_t n, int64_
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
   if ((rc = need_buffers(q, c, out_idx, out_score))) return rc;
-  if (compute == PMM_COMPUTE_BF16 && (rc = bf16_limits(d, k, n))) return rc;
   {
     // a device list (pmm_set_devices): the corpus row-sharded over it, one
     // shard per listed device (at most n shards), results merged on the first
@@ -2192,14 +2240,14 @@ int pmm_topk_bf16_device(const uint16_t *q, int64_t ldq, int64_t m, const uint16
                          int64_t ldc, int64_t n, int64_t d, int64_t k, int metric,
                          uint32_t index_base, uint32_t *out_idx, float *out_score,
                          void *workspace, size_t workspace_bytes, void *stream) {
-  int rc = validate_sizes(m, n, d, k, true, true);
+  // (k > n only where the fused path pads short lists, as for f32)
+  int rc = validate_sizes(m, n, d, k, true, k <= kFusedMaxK);
   if (rc) return rc;
   if ((rc = check_metric(metric))) return rc;
   if (m == 0 || k == 0) return PMM_OK;
   if (n == 0) return fail(PMM_ERR_ARG, "Empty series");
   if (d == 0) return fail(PMM_ERR_ARG, "Zero-dimensional vectors");
   if ((rc = need_buffers(q, c, out_idx, out_score))) return rc;
-  if ((rc = bf16_limits(d, k, n))) return rc;
   const int64_t dp = cdiv(d, kBf16DAlign) * kBf16DAlign;
   if (ldq % 8 != 0 || ldc % 8 != 0 || ldq < dp || ldc < dp || ((uintptr_t)q & 15) ||
       ((uintptr_t)c & 15))

@@ -179,6 +179,9 @@ hipError_t launch_ff_bucket(const GemmF32Args &a, unsigned *fb_count, int *fb_ro
 // d..ldd-1 zero-filled.
 hipError_t launch_f32_to_bf16(const float *src, int64_t rows, int64_t d, int64_t lds, uint16_t *dst,
                               int64_t ldd, hipStream_t s);
+// bf16 rows -> f32 rows (exact), columns d..ldd-1 zero-filled
+hipError_t launch_bf16_to_f32(const uint16_t *src, int64_t rows, int64_t d, int64_t lds, float *dst, int64_t ldd,
+                              hipStream_t s);
 hipError_t launch_norms_bf16(const uint16_t *a, int64_t rows, int64_t d, int64_t ld, int squared,
                              float *out, float *inv, hipStream_t s);
 size_t merge_lds_bytes_per_wave(int P);

@@ -2061,16 +2061,20 @@ hipError_t launch_merge(const MergeArgs &a0, int loader, hipStream_t s) {
                       !(getenv("PMM_MERGE_SORTED") && atoi(getenv("PMM_MERGE_SORTED")) == 0);
   // 5..8 sorted lists (the 8-GPU root merge): the k-way kernel, 8 rows per
   // wave (PMM_MERGE_KWAY=0: the prefix fast path instead)
-  if (sorted && a.S >= 5 && a.S <= 8 && a.k_out <= 8 * kKwayP &&
+  // Staged prefix 24 entries per list, 4 waves per block (12 waves per CU by
+  // LDS): at configs[4]'s root merge (8 x 1M x 100, alternated on one box,
+  // profiles/r6_merge/kway_ab.txt) 1.725 ms against 1.793 (24, 2 waves),
+  // 1.933-1.939 (32 entries) and 2.070 for the prefix fast path alone.  A
+  // list past 24 of a row's answer sends that row to the general path.
+  // (PMM_KWAY_P = 32 / PMM_KWAY_WPB = 2: the A/B alternatives.)
+  static const int kp = getenv("PMM_KWAY_P") ? atoi(getenv("PMM_KWAY_P")) : 24;
+  if (sorted && a.S >= 5 && a.S <= 8 && a.k_out <= 8 * (kp == 32 ? 32 : 24) &&
       !(getenv("PMM_MERGE_KWAY") && atoi(getenv("PMM_MERGE_KWAY")) == 0) &&
-      (size_t)MPN(a.P) * 8 <= (size_t)64 * kKwayP * 8) {
-    // (PMM_KWAY_P = 24 / PMM_KWAY_WPB = 4: A/B knobs -- fewer staged
-    // entries per list, more waves per block)
-    static const int kp = getenv("PMM_KWAY_P") ? atoi(getenv("PMM_KWAY_P")) : 32;
-    static const int wpb = getenv("PMM_KWAY_WPB") ? atoi(getenv("PMM_KWAY_WPB")) : 2;
+      (size_t)MPN(a.P) * 8 <= (size_t)64 * (kp == 32 ? 32 : 24) * 8) {
+    static const int wpb = getenv("PMM_KWAY_WPB") ? atoi(getenv("PMM_KWAY_WPB")) : 4;
     const int rows_per_block = 8 * wpb;
     const unsigned grid = (unsigned)((a.M + rows_per_block - 1) / rows_per_block);
-    if (kp == 24 && (size_t)MPN(a.P) * 8 <= (size_t)64 * 24 * 8) {
+    if (kp != 32) {
       if (wpb == 4) (void)hipFuncSetAttribute((const void *)kway_merge_kernel<24>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       kway_merge_kernel<24><<<grid, 64 * wpb, (size_t)wpb * 64 * 24 * 8, s>>>(a);
     } else {

@@ -57,7 +57,8 @@ def topk(queries: np.ndarray, corpus: np.ndarray, k: int, metric: Metric = "cosi
     (src/matmul.rs:427), scores widened to f64 (src/matmul.rs:447).
     compute="bf16" (an extension, not in the reference): f32 inputs rounded to
     bf16 on the device, bf16 MFMA with f32 accumulation (include/pmm.h
-    PMM_COMPUTE_BF16: d <= 768, k <= 960)."""
+    PMM_COMPUTE_BF16: the bf16 kernels up to d = 768 and k = 960, the rounded
+    rows widened to f32 beyond)."""
     q = np.asarray(queries)
     c = np.asarray(corpus)
     if compute not in ("f32", "bf16"):

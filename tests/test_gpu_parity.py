@@ -1190,17 +1190,42 @@ def test_compaction_trigger_leaves_lists_unchanged(pmm, metric, monkeypatch):
         assert np.array_equal(np.asarray(got_f[1], np.float64), np.asarray(ref_f[1], np.float64)), (metric, t)
 
 
-def test_bf16_limits_raise(pmm):
+@pytest.mark.parametrize("d,k", [(800, 50), (1024, 100), (300, 1000), (1024, 1500)])
+@pytest.mark.parametrize("metric", ["cosine", "euclidean"])
+def test_bf16_beyond_kernel_limits_widened(pmm, d, k, metric):
+    # bf16 compute past the bf16 kernels' limits (d > 768:
+    # configs[4]'s 1024; k > 960) runs on the rounded rows widened to f32, so
+    # it equals the f32 path on the bf16-rounded inputs bit for bit -- and
+    # through the device API with a caller's workspace of the size
+    # pmm_topk_workspace_bytes names
+    import torch
+
     n = _native()
-    q = np.zeros((2, 800), np.float32)
-    with pytest.raises(n.PmmError) as e:
-        n.topk_host(q, q, 1, 0, compute=n.COMPUTE_BF16)
-    assert e.value.code == n.PMM_ERR_UNSUPPORTED and "d <= 768" in str(e.value)
-    q = np.ones((2, 8), np.float32)
-    c = np.ones((1000, 8), np.float32)
-    with pytest.raises(n.PmmError) as e:
-        n.topk_host(q, c, 961, 0, compute=n.COMPUTE_BF16)
-    assert e.value.code == n.PMM_ERR_UNSUPPORTED
+    rs = np.random.RandomState(d + k)
+    q = rs.randn(70, d).astype(np.float32)
+    c = rs.randn(3000, d).astype(np.float32)
+    got = n.topk_host(q, c, k, METRICS[metric], compute=n.COMPUTE_BF16)
+    qr = torch.from_numpy(q).to(torch.bfloat16).float().numpy()
+    cr = torch.from_numpy(c).to(torch.bfloat16).float().numpy()
+    want = n.topk_host(qr, cr, k, METRICS[metric])
+    assert np.array_equal(got[0], want[0])
+    assert np.array_equal(got[1].view(np.uint32), want[1].view(np.uint32))
+    dev = torch.device("cuda:0")
+    db = (d + 127) // 128 * 128
+    tq = torch.zeros((70, db), dtype=torch.bfloat16, device=dev)
+    tc = torch.zeros((3000, db), dtype=torch.bfloat16, device=dev)
+    tq[:, :d] = torch.from_numpy(q).to(dev).to(torch.bfloat16)
+    tc[:, :d] = torch.from_numpy(c).to(dev).to(torch.bfloat16)
+    wb = n.workspace_bytes(70, 3000, db, k, METRICS[metric], n.COMPUTE_BF16)
+    ws = torch.empty(wb, dtype=torch.uint8, device=dev)
+    oi = torch.empty((70, k), dtype=torch.int32, device=dev)
+    osc = torch.empty((70, k), dtype=torch.float32, device=dev)
+    n.topk_bf16_device(tq.data_ptr(), db, 70, tc.data_ptr(), db, 3000, d, k, METRICS[metric], oi.data_ptr(),
+                       osc.data_ptr(), workspace=ws.data_ptr(), workspace_bytes=wb,
+                       stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(oi.cpu().numpy().view(np.uint32), want[0])
+    assert np.array_equal(osc.cpu().numpy().view(np.uint32), want[1].view(np.uint32))
 
 
 def test_bf16_numpy_api_and_sharded_runner(pmm):
