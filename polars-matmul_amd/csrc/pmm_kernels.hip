@@ -1191,7 +1191,6 @@ __global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
 // instructions per step for 8 rows at once, no selection and no sort: the
 // lists' order is the merge's order.
 // ===========================================================================
-constexpr int kKwayP = 32;  // staged entries per (row, list), the largest instantiation
 __device__ __forceinline__ u64 dpp_u64(u64 v, int ctrl_sel) {
   uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
   if (ctrl_sel == 0) {  // row_half_mirror: lane i of each 8 <- lane 7 - i
