@@ -236,6 +236,7 @@ struct Plan {
   int variant = 0;
   int QB = 0, T = 0, tps = 0, S = 0, units = 0, grid = 0, capg = 0, P = 0, qb_full = 0;
   int ctrig = 0;  // compaction trigger (GemmF32Args::ctrig)
+  int segs = 0;   // candidate segments per row (S, or 2 S for the column-split f32 variant)
   size_t off_counter = 0, off_gthr = 0, off_cnt = 0, off_cand = 0, off_qn = 0, off_cn = 0;
   size_t off_wq = 0;
   // fire-and-forget bf16 kernel (variant -6): guess sample size and rank,
@@ -287,7 +288,8 @@ int choose_variant(int mode, int capg, int64_t m = 1 << 30, int64_t n = 1 << 30,
   // (read per call, so a test can force each variant in turn)
   const char *ev = getenv("PMM_GEMM_VARIANT");
   const int env = ev ? atoi(ev) : -1;
-  if (env >= 0 && env < 5 && gemm_f32_lds_bytes(env, mode, capg) <= 160 * 1024) return env;
+  if (env >= 0 && env < 6 && (env != 5 || mode == 0) && gemm_f32_lds_bytes(env, mode, capg) <= 160 * 1024)
+    return env;
   if (cdiv(m, 256) * cdiv(n, 256) < 4 * (int64_t)cus && gemm_f32_lds_bytes(0, mode, capg) <= 160 * 1024) {
     // 128 x 128 tiles, or for the fused top-k 128 x 64 (variant 4) when its
     // finer units give a shorter makespan: per unit, tps tiles of bn / 128
@@ -445,16 +447,17 @@ int plan_topk(int64_t m, int64_t n, int64_t d, int64_t k, int metric, int cus, P
   off += 256;
   p.off_gthr = off;
   off = al256(off + (size_t)m * 8);
+  p.segs = p.S * (bf16 ? 1 : gemm_f32_segs(p.variant));
   p.off_cnt = off;
-  off = al256(off + (size_t)m * p.S * 4);
+  off = al256(off + (size_t)m * p.segs * 4);
   p.off_cand = off;
-  off = al256(off + (size_t)m * p.S * p.capg * 8);
+  off = al256(off + (size_t)m * p.segs * p.capg * 8);
   p.off_qn = off;  // [norms m | inverse norms m]
   off = al256(off + (metric != kMetricDot ? (size_t)m * 8 : 0));
   p.off_cn = off;  // [norms n | inverse norms n]
   off = al256(off + (metric != kMetricDot ? (size_t)n * 8 : 0));
   p.off_wq = off;  // f32 kernel: per-wave survivor queues, grid x waves x (32 x BN) u64
-  off = al256(off + (bf16 ? 0 : (size_t)p.grid * (bm / 32) * 32 * bn * 8));
+  off = al256(off + (bf16 ? 0 : (size_t)p.grid * gemm_f32_nw(p.variant) * 32 * bn * 8));
   if (ffk) {
     p.off_ffcnt = off;  // [units][4 waves]
     off = al256(off + (size_t)p.units * 4 * 4);
@@ -593,11 +596,11 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
   a.ctrig = p.ctrig;
   a.metric = f.metric;
   a.QB = p.QB;
-  a.S = p.S;
   a.tps = p.tps;
   a.ntiles = p.T;
   a.units = (int)units;
   a.qb_full = p.qb_full;
+  a.S = p.segs;  // (the kernel indexes candidate segments with it)
   a.counter = (unsigned *)(w + p.off_counter);
 #ifdef PMM_LAB
   {
@@ -650,7 +653,7 @@ hipError_t run_fused_f32(const FusedF32 &f, const Plan &p, char *w, uint32_t ind
   ma.gthr = a.gthr;
   ma.capg = p.capg;
   ma.M = (int)f.m;
-  ma.S = p.S;
+  ma.S = p.segs;
   ma.k_out = (int)f.k;
   ma.P = p.P;
   ma.metric = f.metric;
@@ -2112,12 +2115,12 @@ int pmm_topk_merge_bytes(const void *workspace, int64_t m, int64_t n, int64_t d,
   plan_topk(m, n, d, k, metric, cus, p, compute);
   // the merge reads every row's split counts and shared threshold, the
   // candidates the GEMM left, and writes the m x k (index, score) lists
-  std::vector<unsigned> cnt((size_t)m * p.S);
+  std::vector<unsigned> cnt((size_t)m * p.segs);
   HIP_TRY(hipMemcpy(cnt.data(), (const char *)workspace + p.off_cnt, cnt.size() * 4,
                     hipMemcpyDeviceToHost));
   uint64_t cands = 0;
   for (unsigned c : cnt) cands += std::min<unsigned>(c, (unsigned)p.capg);
-  *bytes = (uint64_t)m * p.S * 4 + cands * 8 + (uint64_t)m * 8 + (uint64_t)m * k * 8;
+  *bytes = (uint64_t)m * p.segs * 4 + cands * 8 + (uint64_t)m * 8 + (uint64_t)m * k * 8;
   return PMM_OK;
 }
 

@@ -118,11 +118,14 @@ hipError_t launch_norms_f32(const float *a, int64_t rows, int64_t d, int64_t ld,
 hipError_t launch_norms_f64(const double *a, int64_t rows, int64_t d, int64_t ld, int squared,
                             double *out, hipStream_t s);
 // Tile-shape variant of the f32 GEMM (see pmm_kernels.hip): 0 = 128x128,
-// 1 = 128x256, 2 = 256x128 (2 waves/SIMD), 3 = 256x256 (2 waves/SIMD).
+// 1 = 128x256, 2 = 256x128 (2 waves/SIMD), 3 = 256x256 (2 waves/SIMD),
+// 4 = 128x64, 5 = 128x64 column-split (2 waves/SIMD, fused top-k only).
 // mode 0 = fused top-k, 1 = store.  grid = number of persistent workgroups.
 hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid, hipStream_t s);
 int gemm_f32_bm(int variant);   // query rows per workgroup
 int gemm_f32_bn(int variant);   // corpus columns per tile
+int gemm_f32_nw(int variant);   // waves per workgroup
+int gemm_f32_segs(int variant); // candidate segments per (row, corpus split): 2 for the column split
 size_t gemm_f32_lds_bytes(int variant, int mode, int capg);
 hipError_t launch_merge(const MergeArgs &a, int loader, hipStream_t s);
 // Threshold seeding: gthr[row] = (k-th best composite of the row's ns

@@ -96,22 +96,32 @@ constexpr int kF32Stages = 2;
 template <int NB, int NW, bool AK = false>
 struct GemmShape {
   static constexpr int NS = kF32Stages;
+  // CSP (column split; variant 5): 8 waves, 2 per SIMD, in pairs -- waves w
+  // and w + 4 own the same 32 query rows (row group w & 3) and one 32-column
+  // half of the tile each, with separate top-k state (candidate segments
+  // 2 s + half).  One wave per SIMD left the K step's LDS latency and the
+  // tile epilogue uncovered at the reference's own size; a partner wave on
+  // the SIMD issues MFMAs meanwhile.
+  static constexpr bool CSP = NB == 2 && NW == 8;
+  static constexpr int RG = CSP ? NW / 2 : NW;      // row groups of 32
+  static constexpr int NBW = CSP ? NB / 2 : NB;     // 32-column blocks per wave
   static constexpr int BN = 32 * NB;                // corpus columns per tile
-  static constexpr int BM = 32 * NW;                // query rows per workgroup
-  static constexpr int A_BYTES = NW * 4096;         // NW waves x 32 rows x 128 B
+  static constexpr int BM = 32 * RG;                // query rows per workgroup
+  static constexpr int RS = 32 * NW;                // per-wave row-state slots
+  static constexpr int A_BYTES = RG * 4096;         // RG row groups x 32 rows x 128 B
   static constexpr int B_BYTES = BN * 128;          // BN rows x 128 B
   static constexpr int A_IN_STAGE = AK ? 0 : A_BYTES;
   static constexpr int STAGE = A_IN_STAGE + B_BYTES;
   static constexpr int BPIECES = B_BYTES / 1024 / NW;  // 1 KiB LDS-DMA pieces per wave
   static constexpr int OFF_THR = NS * STAGE;
-  static constexpr int OFF_CNT = OFF_THR + BM * 8;
-  static constexpr int OFF_QEX = OFF_CNT + BM * 4;   // exact row norm (epilogue)
-  static constexpr int OFF_LO = OFF_QEX + BM * 4;    // pre-filter bound per row
-  static constexpr int OFF_CV = OFF_LO + BM * 4;     // column factors, NS tiles
+  static constexpr int OFF_CNT = OFF_THR + RS * 8;
+  static constexpr int OFF_QEX = OFF_CNT + RS * 4;   // exact row norm (epilogue)
+  static constexpr int OFF_LO = OFF_QEX + RS * 4;    // pre-filter bound per row
+  static constexpr int OFF_CV = OFF_LO + RS * 4;     // column factors, NS tiles
   // column norms of the exact re-scores, NS tiles, and the survivor queue in
   // LDS: the small variants only (the 256 x 256 one's carve has no room left
   // at k = 100; its survivors are rare after a unit's first tiles)
-  static constexpr bool CNL = NB <= 4 && NW == 4;
+  static constexpr bool CNL = NB <= 4 && (NW == 4 || CSP);
   static constexpr int OFF_CN = OFF_CV + NS * BN * 4;
   static constexpr int OFF_UNIT = OFF_CN + (CNL ? NS * BN * 4 : 0);
   static constexpr int OFF_SCR = OFF_UNIT + 16;
@@ -123,23 +133,29 @@ struct GemmShape {
 //   0: NB=4 NW=4 (128 x 128, 1 wave/SIMD)   1: NB=8 NW=4 (128 x 256)
 //   2: NB=4 NW=8 (256 x 128, 2 waves/SIMD)  3: NB=8 NW=8 (256 x 256)
 //   4: NB=2 NW=4 (128 x 64, 1 wave/SIMD: finer units for small problems)
-constexpr int kGemmVariants = 5;
-constexpr int kVarNB[kGemmVariants] = {4, 8, 4, 8, 2};
-constexpr int kVarNW[kGemmVariants] = {4, 4, 8, 8, 4};
+//   5: NB=2 NW=8 (128 x 64, 2 waves/SIMD splitting the columns: GemmShape::CSP)
+constexpr int kGemmVariants = 6;
+constexpr int kVarNB[kGemmVariants] = {4, 8, 4, 8, 2, 2};
+constexpr int kVarNW[kGemmVariants] = {4, 4, 8, 8, 4, 8};
+constexpr int kVarRG[kGemmVariants] = {4, 4, 8, 8, 4, 4};  // row groups of 32
 
-int gemm_f32_bm(int variant) { return 32 * kVarNW[variant]; }
+int gemm_f32_bm(int variant) { return 32 * kVarRG[variant]; }
 int gemm_f32_bn(int variant) { return 32 * kVarNB[variant]; }
+int gemm_f32_nw(int variant) { return kVarNW[variant]; }
+int gemm_f32_segs(int variant) { return variant == 5 ? 2 : 1; }
 
 // bytes at ns LDS stages; the fit checks use the double-buffered carve
 // (ks_resident > 0: the AK carve, query rows of ks_resident K steps after it)
 static size_t gemm_f32_lds_bytes_ak(int variant, int mode, int capg, int ks_resident) {
   const int ns = kF32Stages;
   const int nb = kVarNB[variant], nw = kVarNW[variant];
-  const size_t a_bytes = (size_t)nw * 4096;
+  const bool csp = variant == 5;  // GemmShape::CSP: no compaction scratch (capg <= 512)
+  const size_t a_bytes = (size_t)kVarRG[variant] * 4096;
   const size_t stage = (ks_resident ? 0 : a_bytes) + (size_t)32 * nb * 128;
-  const bool cnl = nb <= 4 && nw == 4;  // GemmShape::CNL
+  const bool cnl = nb <= 4 && (nw == 4 || csp);  // GemmShape::CNL
   const size_t fixed = ns * stage + (size_t)32 * nw * 20 + (size_t)(cnl ? 2 : 1) * ns * 32 * nb * 4 + 16;
-  return fixed + (mode == 0 ? (size_t)nw * capg * 8 : 0) + (size_t)ks_resident * a_bytes;
+  if (csp && capg > 512) return size_t(1) << 30;  // (its compactions select: capg <= 512 only)
+  return fixed + (mode == 0 && !csp ? (size_t)nw * capg * 8 : 0) + (size_t)ks_resident * a_bytes;
 }
 size_t gemm_f32_lds_bytes(int variant, int mode, int capg) { return gemm_f32_lds_bytes_ak(variant, mode, capg, 0); }
 
@@ -183,11 +199,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  constexpr bool CSP = G::CSP;
+  constexpr int NBW = G::NBW;
+  const int rg = CSP ? (wid & (G::RG - 1)) : wid;  // this wave's row group
+  const int half = CSP ? (wid / G::RG) : 0;        // CSP: this wave's column half of the tile
   const int r32 = lane & 31, h = lane >> 5;
   const int KS = a.D >> 5;
-  u64 *scr = (u64 *)(smem + G::OFF_SCR) + (size_t)wid * a.capg;
-  // AK: the resident query rows, [KS][NW waves][32 rows x 128 B]
-  char *a_res = smem + G::OFF_SCR + (MODE == 0 ? (size_t)NW * a.capg * 8 : 0);
+  // (CSP: no compaction scratch -- capg <= 512 selects in registers)
+  u64 *scr = CSP ? nullptr : (u64 *)(smem + G::OFF_SCR) + (size_t)wid * a.capg;
+  // AK: the resident query rows, [KS][RG row groups][32 rows x 128 B]
+  char *a_res = smem + G::OFF_SCR + (MODE == 0 && !CSP ? (size_t)NW * a.capg * 8 : 0);
   // the survivor queue's first a.qcap entries per wave (the rest: a.wq)
   u64 *lq = (u64 *)(a_res + (AK ? (size_t)KS * G::A_BYTES : 0)) + (size_t)wid * a.qcap;
   u64 *thr_w = thr_l + wid * 32;
@@ -212,7 +233,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   // a row (physical chunk p>>2, element j = p&3) holds logical chunk
   // ch = (p>>2) ^ swizzle, i.e. k = 8*(ch>>1) + (ch&1) + 2j.  Plain image
   // (16-byte pieces of 1 KiB = 8 rows): chunk ch of a row at ch ^ swizzle.
-  constexpr int KO = (NB <= 4 && NW == 4) ? PMM_F32_KORDER_SMALL : PMM_F32_KORDER;
+  constexpr int KO = (NB <= 4 && (NW == 4 || CSP)) ? PMM_F32_KORDER_SMALL : PMM_F32_KORDER;
   constexpr bool A_GATHER = KO == 2;
   constexpr bool B_GATHER = KO == 2 || KO == 3;
   constexpr int AP = A_GATHER ? 16 : 4, APIECE = A_GATHER ? 256 : 1024, ADW = A_GATHER ? 4 : 16;
@@ -248,7 +269,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
   }
   // Per-lane LDS read offsets (within a stage).
   const int swz = (r32 >> 1) & 7;
-  const int a_rd = wid * 4096 + r32 * 128;
+  const int a_rd = rg * 4096 + r32 * 128;
   const int b_rd = G::A_IN_STAGE + r32 * 128;
 
   int buf = 0;
@@ -276,7 +297,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       t0 = s * a.tps;
       t1 = min(t0 + a.tps, a.ntiles);
     }
-    const int wrow0 = qb * G::BM + wid * 32;
+    const int wrow0 = qb * G::BM + rg * 32;
+    const int seg = CSP ? 2 * s + half : s;  // this wave's candidate segment
     const __amdgpu_buffer_rsrc_t ra =
         make_rsrc(a.q + (int64_t)wrow0 * a.ldq, (int64_t)min(32, a.M - wrow0) * a.ldq * 4);
 
@@ -316,7 +338,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       constexpr int AS = AK ? 0 : AP;  // A pieces per step in the ring
 #pragma unroll
       for (int i = 0; i < AS; i++)
-        if (i >= lo && i < hi && !skip_a) dma(ra, st + wid * 4096 + i * APIECE, a_voff[i], ADW);
+        if (i >= lo && i < hi && !skip_a && half == 0) dma(ra, st + rg * 4096 + i * APIECE, a_voff[i], ADW);
 #pragma unroll
       for (int i = 0; i < BP; i++)
         if (AS + i >= lo && AS + i < hi) dma(rb, st + G::A_IN_STAGE + (i * NW + wid) * BPIECE, b_voff[i], BDW);
@@ -354,7 +376,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     // cover this wave's DMA issue; its 8 pieces per step go out 4 behind each
     // of the first two MFMA groups: c1 0.141 vs 0.143 ms, c2 0.134 vs 0.136;
     // 2 behind each of four groups 0.146 / 0.139)
-    constexpr int NPART = (NB <= 4 && NW == 4) ? PMM_F32_DMA_PARTS_SMALL : PMM_F32_DMA_PARTS;
+    constexpr int NPART = (NB <= 4 && (NW == 4 || CSP)) ? PMM_F32_DMA_PARTS_SMALL : PMM_F32_DMA_PARTS;
 // The large variants' pre-filter in two passes: per-lane survivor flags with
 // no branches, their OR over the wave, then ballot + append at the flagged
 // positions only (wave-uniform element index).  The one-pass form ran a
@@ -370,7 +392,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
 #ifndef PMM_F32_FRAG_PREFETCH
 #define PMM_F32_FRAG_PREFETCH 1  // (A/B: 0 off, 1 the 128 x 128 variant only, 2 every variant)
 #endif
-    constexpr bool FPF = PMM_F32_FRAG_PREFETCH == 2 || (PMM_F32_FRAG_PREFETCH == 1 && NB <= 4 && NW == 4);
+    constexpr bool FPF = PMM_F32_FRAG_PREFETCH == 2 || (PMM_F32_FRAG_PREFETCH == 1 && NB <= 4 && (NW == 4 || CSP));
     // (one ballot per 32 x 32 block before the per-score ones -- the max of
     // the pre-filter differences -- measured flat at c3 in round 2 and slower
     // at c1 in round 3: 0.083-0.085 vs 0.082 ms,
@@ -380,10 +402,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     if (AK) {
       // the unit's query rows, every K step, once (the unit-start barriers
       // above: every wave is done with the previous unit's rows)
-      for (int ks = 0; ks < KS; ks++)
+      for (int ks = 0; ks < KS && half == 0; ks++)
 #pragma unroll
         for (int i = 0; i < AP; i++) {
-          char *dst = a_res + ks * G::A_BYTES + wid * 4096 + i * APIECE;
+          char *dst = a_res + ks * G::A_BYTES + rg * 4096 + i * APIECE;
           if (ADW == 4)
             __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (LDS_AS void *)dst, 4, a_voff[i], (uint32_t)ks * 128u, 0, 0);
           else
@@ -396,16 +418,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       const uint64_t tl0 = stamp();
       const bool last_tile = (tile + 1) >= t1;
       const __amdgpu_buffer_rsrc_t rbn = last_tile ? rb : rsrc_b(tile + 1);
-      f32x16 acc[NB];
+      f32x16 acc[NBW];
 #pragma unroll
-      for (int c = 0; c < NB; c++) acc[c] = (f32x16){};
+      for (int c = 0; c < NBW; c++) acc[c] = (f32x16){};
       // PMM_F32_DEFER: the last substep(s) of a K step (NB MFMAs each, their
       // operands one A and NB B values) run after the next step's barrier,
       // behind the next step's first fragment reads -- the same MFMA order
       // per accumulator, so the same bits
       constexpr int DN = PMM_F32_DEFER;  // substeps deferred (1 or 2)
       static_assert(DN >= 0 && DN <= 2, "PMM_F32_DEFER: 0, 1 or 2 substeps");
-      float dA[DN > 0 ? DN : 1], dB[DN > 0 ? DN : 1][NB];
+      float dA[DN > 0 ? DN : 1], dB[DN > 0 ? DN : 1][NBW];
       // one K step; DEF: defer its last substep, PREV: run the previous
       // step's deferred substep first (compile-time, so no per-substep branch)
       auto kstep = [&](int ks, auto DEF, auto PREV) __attribute__((always_inline)) {
@@ -421,16 +443,16 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         // a plain image (k = 8qd+4h..+3) two v_permlane32_swap trade the
         // lower half's odd k for the upper half's even k, leaving registers
         // {0,2,1,3} = k pairs (8qd,+1) (8qd+2,+3) (8qd+4,+5) (8qd+6,+7).
-        auto rd_frag = [&](int qd, f32x4 &av, f32x4 (&b)[NB]) __attribute__((always_inline)) {
+        auto rd_frag = [&](int qd, f32x4 &av, f32x4 (&b)[NBW]) __attribute__((always_inline)) {
           const int co = KO == 0 ? 16 * ((4 * h + qd) ^ swz) : 16 * ((2 * qd + h) ^ swz);
           av = *(const f32x4 *)((AK ? a_res + ks * G::A_BYTES : st) + a_rd + co);
 #pragma unroll
-          for (int c = 0; c < NB; c++) b[c] = *(const f32x4 *)(st + b_rd + c * 4096 + co);
+          for (int c = 0; c < NBW; c++) b[c] = *(const f32x4 *)(st + b_rd + (half * NBW + c) * 4096 + co);
         };
         // FPF: group qd + 1's fragments are read before group qd's MFMAs, so
         // only a K step's first group waits on a fresh LDS read (one wave per
         // SIMD has no partner wave to cover that latency)
-        f32x4 avs[FPF ? 2 : 1], bs[FPF ? 2 : 1][NB];
+        f32x4 avs[FPF ? 2 : 1], bs[FPF ? 2 : 1][NBW];
         if (FPF) rd_frag(0, avs[0], bs[0]);
 #pragma unroll
         for (int qd = 0; qd < 4; qd++) {
@@ -440,7 +462,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           }
           if (!FPF) rd_frag(qd, avs[0], bs[0]);
           f32x4 &av = avs[FPF ? (qd & 1) : 0];
-          f32x4(&b)[NB] = bs[FPF ? (qd & 1) : 0];
+          f32x4(&b)[NBW] = bs[FPF ? (qd & 1) : 0];
           constexpr bool A_SWAP = KO == 1 || KO == 3;
           constexpr bool B_SWAP = KO == 1;
           auto kpair = [](f32x4 &x) __attribute__((always_inline)) {
@@ -456,12 +478,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
 #pragma unroll
             for (int j = 0; j < DN; j++)
 #pragma unroll
-              for (int c = 0; c < NB; c++)
+              for (int c = 0; c < NBW; c++)
                 acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(dA[j], dB[j][c], acc[c], 0, 0, 0);
           }
           if (A_SWAP) kpair(av);
 #pragma unroll
-          for (int c = 0; c < NB; c++)
+          for (int c = 0; c < NBW; c++)
             if (B_SWAP) kpair(b[c]);
 #pragma unroll
           for (int jj = 0; jj < 4; jj++) {
@@ -470,10 +492,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             if (decltype(DEF)::value && qd == 3 && jj >= 4 - DN) {
               dA[jj - (4 - DN)] = av[ja];
 #pragma unroll
-              for (int c = 0; c < NB; c++) dB[jj - (4 - DN)][c] = b[c][jb];
+              for (int c = 0; c < NBW; c++) dB[jj - (4 - DN)][c] = b[c][jb];
             } else {
 #pragma unroll
-              for (int c = 0; c < NB; c++)
+              for (int c = 0; c < NBW; c++)
                 acc[c] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[ja], b[c][jb], acc[c], 0, 0, 0);
             }
           }
@@ -513,7 +535,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         // ablation build path: keep the accumulators live, skip the epilogue
         float sink = 0.0f;
 #pragma unroll
-        for (int c = 0; c < NB; c++)
+        for (int c = 0; c < NBW; c++)
 #pragma unroll
           for (int e = 0; e < 16; e++) sink += acc[c][e];
         asm volatile("" ::"v"(sink));
@@ -528,8 +550,8 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
       if (MODE == 1) {
         // ---- store epilogue (.pmm.matmul, or materialised scores) ----
 #pragma unroll
-        for (int c = 0; c < NB; c++) {
-          const int gcol = col0 + 32 * c + r32;
+        for (int c = 0; c < NBW; c++) {
+          const int gcol = col0 + 32 * (half * NBW + c) + r32;
           if (gcol < a.N) {
             const float cv = XFORM ? a.cn[gcol] : 0.0f;
 #pragma unroll
@@ -577,9 +599,10 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           // row's buffer a superset of its top-k above the threshold).
           u64 bits = 0ull;
 #pragma unroll
-          for (int c = 0; c < NB; c++) {
-            const bool cvalid = col0 + 32 * c + r32 < a.N;
-            const float cv = XFORM ? cvt[32 * c + r32] : 0.0f;
+          for (int c = 0; c < NBW; c++) {
+            const int tb = half * NBW + c;  // the 32-column block of the tile
+            const bool cvalid = col0 + 32 * tb + r32 < a.N;
+            const float cv = XFORM ? cvt[32 * tb + r32] : 0.0f;
 #pragma unroll
             for (int e = 0; e < 16; e++)
               if (cvalid && !(prefilter(acc[c][e], cv) < lo[e])) bits |= 1ull << (16 * c + e);
@@ -596,11 +619,12 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           if (bits && PMM_ABL(a.ablate) != 2) {
             int qi = qlen + excl;
 #pragma unroll
-            for (int c = 0; c < NB; c++)
+            for (int c = 0; c < NBW; c++)
 #pragma unroll
               for (int e = 0; e < 16; e++)
                 if ((bits >> (16 * c + e)) & 1ull) {
-                  const uint32_t hi = lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * c) << 5));
+                  const uint32_t hi =
+                      lane_hi + (uint32_t)((e & 3) + 8 * (e >> 2) + ((32 * (half * NBW + c)) << 5));
                   const u64 item = (u64)__float_as_uint(acc[c][e]) | ((u64)hi << 32);
 #if PMM_F32_FLAT_QUEUE
                   // one generic (flat) store, LDS or global by address: no
@@ -621,11 +645,11 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           // block c, two blocks per word), then their OR over the wave -- the
           // positions (c, e) where some lane holds a survivor; only those
           // take the ballot + append below
-          uint32_t fl[(NB + 1) / 2], U[(NB + 1) / 2];
+          uint32_t fl[(NBW + 1) / 2], U[(NBW + 1) / 2];
 #pragma unroll
-          for (int i = 0; i < (NB + 1) / 2; i++) fl[i] = 0u;
+          for (int i = 0; i < (NBW + 1) / 2; i++) fl[i] = 0u;
 #pragma unroll
-          for (int c = 0; c < NB; c++) {
+          for (int c = 0; c < NBW; c++) {
             const float cv = XFORM ? cvt[32 * c + r32] : 0.0f;
             uint32_t f = 0u;
 #pragma unroll
@@ -634,7 +658,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
             fl[c >> 1] |= f << (16 * (c & 1));
           }
 #pragma unroll
-          for (int i = 0; i < (NB + 1) / 2; i++) {
+          for (int i = 0; i < (NBW + 1) / 2; i++) {
             uint32_t x = fl[i];
 #pragma unroll
             for (int off = 32; off; off >>= 1) x |= (uint32_t)__shfl_xor((int)x, off);
@@ -643,7 +667,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
           // pass 2: the flagged positions only, block by block (e is
           // wave-uniform: the accumulator element is read by index)
 #pragma unroll
-          for (int c = 0; c < NB; c++) {
+          for (int c = 0; c < NBW; c++) {
             uint32_t uc = (U[c >> 1] >> (16 * (c & 1))) & 0xFFFFu;
             while (uc) {
               const int e = __builtin_ctz(uc);
@@ -660,7 +684,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
         }
 #else
 #pragma unroll
-          for (int c = 0; c < NB; c++) {
+          for (int c = 0; c < NBW; c++) {
             const int gcol = col0 + 32 * c + r32;
             const bool cvalid = gcol < a.N;
             const float cv = XFORM ? cvt[32 * c + r32] : 0.0f;
@@ -706,7 +730,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
               const u64 comp = ((u64)key << 32) | (u64)(~(uint32_t)gcol);
               if (comp > thr_w[rl]) {
                 const unsigned pos = atomicAdd(&cnt_w[rl], 1u);
-                a.cand[((int64_t)(wrow0 + rl) * a.S + s) * a.capg + pos] = comp;
+                a.cand[((int64_t)(wrow0 + rl) * a.S + seg) * a.capg + pos] = comp;
               }
             }
             // compact every row whose buffer could overflow on the next 64 appends
@@ -719,7 +743,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
               while (need) {
                 const int r = __builtin_ctzll(need);
                 need &= need - 1;
-                compact_row(a, s, wrow0 + r, thr_w + r, cnt_w + r, scr, lane);
+                compact_row(a, seg, wrow0 + r, thr_w + r, cnt_w + r, scr, lane);
               }
               if (lane < 32) lo_w[lane] = prefilter_bound<METRIC>(thr_w[lane], qex_w[lane]);
               wave_sync();
@@ -734,7 +758,7 @@ __global__ __launch_bounds__(NW * 64, NW / 4) void gemm_f32_kernel(GemmF32Args a
     if (MODE == 0) {
       if (lane < 32) {
         const int grow = wrow0 + lane;
-        if (grow < a.M) a.cnt[(int64_t)grow * a.S + s] = cnt_w[lane];
+        if (grow < a.M) a.cnt[(int64_t)grow * a.S + seg] = cnt_w[lane];
       }
     }
   }
@@ -812,6 +836,7 @@ hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid
     case 2: return launch_gemm_f32_v<4, 8>(a, mode, grid, lds, s);
     case 3: return launch_gemm_f32_v<8, 8>(a, mode, grid, lds, s);
     case 4: return launch_gemm_f32_small<2, 4>(a, variant, mode, grid, s);
+    case 5: return mode == 0 ? launch_gemm_f32_small<2, 8>(a, variant, mode, grid, s) : hipErrorInvalidValue;
     default: return hipErrorInvalidValue;
   }
 }

@@ -742,7 +742,7 @@ def test_merge_schedules_same_lists(pmm, flags, shape, monkeypatch):
     assert_bitexact(got[0][rows], got[1][rows], oi, osc, label=f"merge flags {flags}")
 
 
-@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4"])
+@pytest.mark.parametrize("variant", ["0", "1", "2", "3", "4", "5", "5:whole"])
 def test_every_tile_variant_same_lists(pmm, variant, monkeypatch):
     # each f32 tile variant forced in turn (PMM_GEMM_VARIANT, per call): the
     # 128-wide ones with the per-lane flag pre-filter, the 256-wide ones with
@@ -750,6 +750,12 @@ def test_every_tile_variant_same_lists(pmm, variant, monkeypatch):
     # variant returns the default's lists bit for bit, and the oracle's.  A
     # variant whose LDS carve does not hold the candidate buffers of a k
     # falls back to the chosen one (k = 300 on 256 x 256).
+    # ("5": the column split, two waves per SIMD splitting each tile's
+    # columns, two candidate segments per row and split; "5:whole" plans for 4
+    # workgroups so most query blocks run whole)
+    if variant.endswith(":whole"):
+        variant = variant.split(":")[0]
+        monkeypatch.setenv("PMM_CUS", "4")
     rs = np.random.RandomState(41)
     m, N, d = 700, 9001, 80
     q = rs.randn(m, d).astype(np.float32)
