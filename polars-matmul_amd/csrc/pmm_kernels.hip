@@ -880,6 +880,17 @@ hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid
 #ifndef PMM_MERGE_SEL_E
 #define PMM_MERGE_SEL_E 1
 #endif
+// Chunk loads per batch (two batches in flight when pipelined) and the
+// merge kernels' occupancy floor.  The merge is bound by each wave's
+// dependent chain (counts -> chunks -> select -> sort -> write), so waves per
+// SIMD count: at 4 chunks per batch merge_kernel<0> took 80 VGPRs (6 waves);
+// 2 per batch and a 7-wave floor fit it in 72 with no scratch.  Round 6,
+// alternated on one box (profiles/r6_merge/occupancy_ab.txt): c3 0.424 ->
+// 0.401 ms, c4 0.288 -> 0.262, c5_rank 2.55 -> 2.33, c1 equal; 3 per batch
+// the same.  (A floor of 8 spills; a 64-VGPR lab build measured alike.)
+#ifndef PMM_MERGE_MU
+#define PMM_MERGE_MU 2
+#endif
 __device__ inline void wave_sort_desc_u64_pad(u64 *s, int P, int lane) {
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -1047,7 +1058,7 @@ __device__ __forceinline__ void merge_row(const MergeArgs &a, const int rpos, co
     // bandwidth, bounded the per-list loop).  (A flat per-slot loader -- prefix
     // sums + a binary search per slot -- measured the same at c1 and 29%
     // slower at c3.)
-    constexpr int MU = 4;  // (8 and 16 in flight measured the same at c1 and c3)
+    constexpr int MU = PMM_MERGE_MU;  // (see PMM_MERGE_MU; round 3: 8 and 16 in flight alike at c1, c3)
     // (lists [s_lo, s_hi): lane j holds list s_lo + j's length)
     const int nl = (s_lo + lane < s_hi)
                        ? ((LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + s_lo + lane] : a.k_in)
@@ -1167,11 +1178,18 @@ __device__ __forceinline__ void merge_row(const MergeArgs &a, const int rpos, co
     wave_sync();
   }
   if (PMM_ABL(a.ablate) != 1) {
+    // (lab ablate 4: no selection, the first k_out kept; 5: no ranking, slot
+    // order; 6: neither -- benchmarking only, results wrong)
+    if ((PMM_ABL(a.ablate) == 4 || PMM_ABL(a.ablate) == 6) && cnt > a.k_out) cnt = a.k_out;
     if (cnt > a.k_out && a.P <= 512) {
         const CompactOut o = merge_compact(scr, cnt, a.k_out, a.P, T, lane);
         cnt = o.cnt;
         T = o.T;
       }
+    if (PMM_ABL(a.ablate) == 5 || PMM_ABL(a.ablate) == 6) {
+      for (int j = lane; j < a.k_out; j += 64) put(j, (j < cnt) ? scr[MP(j)] : 0ull);
+      return;
+    }
     if (a.k_out <= 128 && cnt <= a.k_out && !a.no_rank) {
       // best-first by rank counting, no sort: each kept key goes to the
       // position = the number of kept keys above it (keys are distinct)
@@ -1192,8 +1210,11 @@ __device__ __forceinline__ void merge_row(const MergeArgs &a, const int rpos, co
   for (int j = lane; j < a.k_out; j += 64) put(j, (j < cnt) ? scr[MP(j)] : 0ull);
 }
 
+#ifndef PMM_MERGE_WAVES
+#define PMM_MERGE_WAVES 7  // (min waves per SIMD: the register budget, see PMM_MERGE_MU)
+#endif
 template <int LOADER, bool SPLIT, bool SORTED = false>
-__global__ __launch_bounds__(256) void merge_kernel(MergeArgs a) {
+__global__ __launch_bounds__(256, PMM_MERGE_WAVES) void merge_kernel(MergeArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wpb = blockDim.x >> 6;
