@@ -931,6 +931,72 @@ __device__ inline void wave_rank2(u64 y0, u64 y1, int n, int &r0, int &r1) {
     r1 += v > y1;
   }
 }
+// Bitonic sort, best first, of 128 keys held two per lane in registers (key
+// i: lane i & 63, y0 for i < 64, y1 above).  Partners at lane distance 1, 2,
+// 4, 8 by DPP (quad_perm, and 4 / 8 as two mirrors: row_half_mirror then
+// quad reverse = lane ^ 4, row_mirror then row_half_mirror = lane ^ 8), 16
+// by ds_bpermute, 32 by v_permlane32_swap, 64 inside the lane: no LDS round
+// trip per stage, against the LDS network's 28 read -> compare -> write
+// stages (wave_sort_desc_u64_pad).  Round 6, alternated on one box
+// (profiles/r6_merge/sort128_ab.txt): merge c3 0.402 -> 0.375 ms, c4 0.267
+// -> 0.231, c5_rank 2.33 -> 2.19; the whole GPU suite passed with every
+// merge forced onto it (PMM_MERGE_RANK=0).
+#ifndef PMM_MERGE_SORT128
+#define PMM_MERGE_SORT128 1
+#endif
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int S>
+__device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v, int lane) {
+  if constexpr (S == 1) return dpp_mov<0xB1>(v);                    // quad_perm [1,0,3,2]
+  else if constexpr (S == 2) return dpp_mov<0x4E>(v);               // quad_perm [2,3,0,1]
+  else if constexpr (S == 4) return dpp_mov<0x1B>(dpp_mov<0x141>(v));  // half mirror, quad reverse
+  else if constexpr (S == 8) return dpp_mov<0x141>(dpp_mov<0x140>(v)); // row mirror, half mirror
+  else if constexpr (S == 16) return (uint32_t)__shfl_xor((int)v, 16);
+  else {
+    // lanes 32-63 of the first operand swap with lanes 0-31 of the second:
+    // r[0] = both halves' low half, r[1] = both halves' high half
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return lane < 32 ? r[1] : r[0];
+  }
+}
+template <int SIZE, int S>
+__device__ __forceinline__ void sort128_step(u64 &y0, u64 &y1, int lane) {
+  // element i keeps the larger of (i, i ^ S) iff (i is the pair's lower) ==
+  // (i's SIZE-block sorts descending: i & SIZE == 0); i = lane + 64 r
+  const bool lower = (lane & S) == 0;
+  const bool d0 = SIZE >= 64 ? true : (lane & SIZE) == 0;
+  const bool d1 = SIZE == 64 ? false : (SIZE > 64 ? true : (lane & SIZE) == 0);
+  auto px = [&](u64 v) __attribute__((always_inline)) {
+    return ((u64)lane_xor_u32<S>((uint32_t)(v >> 32), lane) << 32) | (u64)lane_xor_u32<S>((uint32_t)v, lane);
+  };
+  const u64 p0 = px(y0), p1 = px(y1);
+  const u64 mx0 = y0 > p0 ? y0 : p0, mn0 = y0 > p0 ? p0 : y0;
+  const u64 mx1 = y1 > p1 ? y1 : p1, mn1 = y1 > p1 ? p1 : y1;
+  y0 = (lower == d0) ? mx0 : mn0;
+  y1 = (lower == d1) ? mx1 : mn1;
+}
+template <int SIZE, int S>
+__device__ __forceinline__ void sort128_merge(u64 &y0, u64 &y1, int lane) {
+  sort128_step<SIZE, S>(y0, y1, lane);
+  if constexpr (S > 1) sort128_merge<SIZE, S / 2>(y0, y1, lane);
+}
+__device__ inline void wave_sort128_desc(u64 &y0, u64 &y1, int lane) {
+  sort128_merge<2, 1>(y0, y1, lane);
+  sort128_merge<4, 2>(y0, y1, lane);
+  sort128_merge<8, 4>(y0, y1, lane);
+  sort128_merge<16, 8>(y0, y1, lane);
+  sort128_merge<32, 16>(y0, y1, lane);
+  sort128_merge<64, 32>(y0, y1, lane);
+  // size 128: (i, i + 64) inside the lane, then distances 32 .. 1, all descending
+  const u64 mx = y0 > y1 ? y0 : y1, mn = y0 > y1 ? y1 : y0;
+  y0 = mx;
+  y1 = mn;
+  sort128_merge<128, 32>(y0, y1, lane);
+}
+
 // the k best of the cnt (<= 64 E) keys in scr, unordered, to its front.
 // The raised threshold comes back by value with the count: a threshold the
 // callee wrote through a pointer lived in scratch memory, and every scratch
@@ -1188,6 +1254,14 @@ __device__ __forceinline__ void merge_row(const MergeArgs &a, const int rpos, co
       }
     if (PMM_ABL(a.ablate) == 5 || PMM_ABL(a.ablate) == 6) {
       for (int j = lane; j < a.k_out; j += 64) put(j, (j < cnt) ? scr[MP(j)] : 0ull);
+      return;
+    }
+    if (PMM_MERGE_SORT128 && a.k_out <= 128 && cnt <= 128 && a.no_rank) {
+      u64 y0 = lane < cnt ? scr[MP(lane)] : 0ull;
+      u64 y1 = 64 + lane < cnt ? scr[MP(64 + lane)] : 0ull;
+      wave_sort128_desc(y0, y1, lane);  // (empty slots, 0, sort last)
+      if (lane < a.k_out) put(lane, y0);
+      if (64 + lane < a.k_out) put(64 + lane, y1);
       return;
     }
     if (a.k_out <= 128 && cnt <= a.k_out && !a.no_rank) {
