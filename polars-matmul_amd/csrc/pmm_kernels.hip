@@ -1852,9 +1852,24 @@ __host__ __device__ constexpr size_t lds_bytes(int dp) {
 static_assert((size_t)RM * NSM * 8 <= (size_t)2 * NSM * CS * 4, "keys alias the chunk buffers");
 }  // namespace seedm
 
+#ifdef PMM_SEED_STAMPS
+// (lab only: per-block phase clocks of the MFMA seed blocks, read back by
+// pmm_lab_seed_stamps; divergent lane-0 vector stores)
+__device__ unsigned long long g_seed_st[1024][8];
+#define SEED_ST(i)                                                          \
+  do {                                                                     \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();            \
+    if (threadIdx.x == 0 && b < 1024) g_seed_st[b][i] = t_;                \
+  } while (0)
+#else
+#define SEED_ST(i) \
+  do {             \
+  } while (0)
+#endif
 template <int METRIC>
 __device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned b, char *smem) {
   using namespace seedm;
+  SEED_ST(0);
   constexpr bool XFORM = METRIC != kMetricDot;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int dp = a.dp, d = a.d, m = a.m;
@@ -1898,6 +1913,7 @@ __device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned 
   }
   store_chunk(0, v[0]);
   __syncthreads();
+  SEED_ST(1);
   const int g4 = lane >> 4, l16 = lane & 15;
   const int col0 = 16 * NCH * w + l16;  // chain c: column col0 + 16 c
   const int d8 = d & ~7;
@@ -1946,6 +1962,7 @@ __device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned 
       __syncthreads();
     }
   }
+  SEED_ST(2);
   if (XFORM && tid < NSM) {
     float sum = 0.0f;
     sum = sum + (p[0] + p[4]);
@@ -1961,6 +1978,7 @@ __device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned 
   }
   if (XFORM && w < RM / 8) norms_rows<float, float>(qs, RM, d, QS, a.squared, qn_s, nullptr, tid);
   __syncthreads();
+  SEED_ST(3);
   // D of the 16x16x4: lane holds rows 4 (lane >> 4) + i of its column
 #pragma unroll
   for (int i = 0; i < 4; i++) {
@@ -1976,6 +1994,7 @@ __device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned 
     }
   }
   __syncthreads();
+  SEED_ST(4);
   for (int rr = w; rr < RM; rr += NT / 64) {
     const int row = row0 + rr;
     if (row >= m) return;
@@ -1992,6 +2011,7 @@ __device__ __forceinline__ void seed_mfma_block(const PrologueArgs &a, unsigned 
     const u64 th = seed_threshold<4>(x, a.k);  // a lower bound of the row's final k-th
     if (lane == 0) a.gthr[row] = th;
   }
+  SEED_ST(5);
 }
 
 template <int METRIC>
@@ -2023,6 +2043,11 @@ __global__ __launch_bounds__(seedm::NT) void prologue_mfma_kernel(PrologueArgs a
   }
 }
 
+#ifdef PMM_SEED_STAMPS
+extern "C" int pmm_lab_seed_stamps(unsigned long long *out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_seed_st), (size_t)n * 8 * sizeof(unsigned long long));
+}
+#endif
 template <int METRIC>
 static hipError_t launch_prologue_mfma_t(const PrologueArgs &a, unsigned grid, hipStream_t s) {
   static bool attr = false;
