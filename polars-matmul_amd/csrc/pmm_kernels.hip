@@ -891,9 +891,6 @@ hipError_t launch_gemm_f32(const GemmF32Args &a, int variant, int mode, int grid
 #ifndef PMM_MERGE_MU
 #define PMM_MERGE_MU 2
 #endif
-#ifndef PMM_MERGE_MU_SPLIT
-#define PMM_MERGE_MU_SPLIT 2
-#endif
 __device__ inline void wave_sort_desc_u64_pad(u64 *s, int P, int lane) {
   for (int size = 2; size <= P; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -1127,7 +1124,7 @@ __device__ __forceinline__ void merge_row(const MergeArgs &a, const int rpos, co
     // bandwidth, bounded the per-list loop).  (A flat per-slot loader -- prefix
     // sums + a binary search per slot -- measured the same at c1 and 29%
     // slower at c3.)
-    constexpr int MU = SPLIT ? PMM_MERGE_MU_SPLIT : PMM_MERGE_MU;  // (see PMM_MERGE_MU)
+    constexpr int MU = PMM_MERGE_MU;  // (see PMM_MERGE_MU; at c1's split rows 2, 4 and 8 measured alike)
     // (lists [s_lo, s_hi): lane j holds list s_lo + j's length)
     const int nl = (s_lo + lane < s_hi)
                        ? ((LOADER == 0) ? (int)a.cnt[(int64_t)row * a.S + s_lo + lane] : a.k_in)
@@ -1291,7 +1288,7 @@ __device__ __forceinline__ void merge_row(const MergeArgs &a, const int rpos, co
 #define PMM_MERGE_WAVES 7  // (min waves per SIMD: the register budget, see PMM_MERGE_MU)
 #endif
 template <int LOADER, bool SPLIT, bool SORTED = false>
-__global__ __launch_bounds__(256, SPLIT ? 1 : PMM_MERGE_WAVES) void merge_kernel(MergeArgs a) {
+__global__ __launch_bounds__(256, PMM_MERGE_WAVES) void merge_kernel(MergeArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wpb = blockDim.x >> 6;
