@@ -940,13 +940,18 @@ __device__ inline void wave_rank2(u64 y0, u64 y1, int n, int &r0, int &r1) {
 // stages (wave_sort_desc_u64_pad).  Round 6, alternated on one box
 // (profiles/r6_merge/sort128_ab.txt): merge c3 0.402 -> 0.375 ms, c4 0.267
 // -> 0.231, c5_rank 2.33 -> 2.19; the whole GPU suite passed with every
-// merge forced onto it (PMM_MERGE_RANK=0).
+// merge forced onto it (PMM_MERGE_RANK=0).  The compare-exchange as a lane
+// mask (below) and bound_ctrl moves: 0.377 -> 0.329 at c3, 0.222 -> 0.178
+// at c4, 2.13 -> 1.61 at c5_rank (profiles/r6_merge/sort128_mask_ab.txt).
 #ifndef PMM_MERGE_SORT128
 #define PMM_MERGE_SORT128 1
 #endif
+// (every permutation used here gives every lane a valid source, so
+// bound_ctrl costs nothing and spares update_dpp's copy of an old value:
+// kway_merge_kernel 85 -> 78 VGPRs)
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_mov(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
 template <int S>
 __device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v, int lane) {
@@ -962,21 +967,32 @@ __device__ __forceinline__ uint32_t lane_xor_u32(uint32_t v, int lane) {
     return lane < 32 ? r[1] : r[0];
   }
 }
+// element i keeps the larger of (i, i ^ S) iff (i is the pair's lower) ==
+// (i's SIZE-block sorts descending: i & SIZE == 0); i = lane + 64 r.  As a
+// compile-time lane mask per register: one compare into a lane mask, one
+// scalar xor with it, two selects per key (against two selects per max and
+// per min and a third pair to choose between them).
+template <int SIZE, int S, int R>
+constexpr unsigned long long sort128_keepmax() {
+  unsigned long long m = 0;
+  for (int l = 0; l < 64; l++) {
+    const bool lower = (l & S) == 0;
+    const bool d = SIZE > 64 ? true : (SIZE == 64 ? R == 0 : (l & SIZE) == 0);
+    if (lower == d) m |= 1ull << l;
+  }
+  return m;
+}
 template <int SIZE, int S>
 __device__ __forceinline__ void sort128_step(u64 &y0, u64 &y1, int lane) {
-  // element i keeps the larger of (i, i ^ S) iff (i is the pair's lower) ==
-  // (i's SIZE-block sorts descending: i & SIZE == 0); i = lane + 64 r
-  const bool lower = (lane & S) == 0;
-  const bool d0 = SIZE >= 64 ? true : (lane & SIZE) == 0;
-  const bool d1 = SIZE == 64 ? false : (SIZE > 64 ? true : (lane & SIZE) == 0);
   auto px = [&](u64 v) __attribute__((always_inline)) {
     return ((u64)lane_xor_u32<S>((uint32_t)(v >> 32), lane) << 32) | (u64)lane_xor_u32<S>((uint32_t)v, lane);
   };
   const u64 p0 = px(y0), p1 = px(y1);
-  const u64 mx0 = y0 > p0 ? y0 : p0, mn0 = y0 > p0 ? p0 : y0;
-  const u64 mx1 = y1 > p1 ? y1 : p1, mn1 = y1 > p1 ? p1 : y1;
-  y0 = (lower == d0) ? mx0 : mn0;
-  y1 = (lower == d1) ? mx1 : mn1;
+  // take the partner's key where (mine is larger) != (I keep the larger)
+  const u64 t0 = __ballot(y0 > p0) ^ sort128_keepmax<SIZE, S, 0>();
+  const u64 t1 = __ballot(y1 > p1) ^ sort128_keepmax<SIZE, S, 1>();
+  y0 = __builtin_amdgcn_inverse_ballot_w64(t0) ? p0 : y0;
+  y1 = __builtin_amdgcn_inverse_ballot_w64(t1) ? p1 : y1;
 }
 template <int SIZE, int S>
 __device__ __forceinline__ void sort128_merge(u64 &y0, u64 &y1, int lane) {
@@ -1314,14 +1330,14 @@ __global__ __launch_bounds__(256, PMM_MERGE_WAVES) void merge_kernel(MergeArgs a
 __device__ __forceinline__ u64 dpp_u64(u64 v, int ctrl_sel) {
   uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
   if (ctrl_sel == 0) {  // row_half_mirror: lane i of each 8 <- lane 7 - i
-    lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x141, 0xF, 0xF, false);
-    hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x141, 0xF, 0xF, false);
+    lo = dpp_mov<0x141>(lo);
+    hi = dpp_mov<0x141>(hi);
   } else if (ctrl_sel == 1) {  // quad_perm [2,3,0,1]: lane xor 2
-    lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x4E, 0xF, 0xF, false);
-    hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x4E, 0xF, 0xF, false);
+    lo = dpp_mov<0x4E>(lo);
+    hi = dpp_mov<0x4E>(hi);
   } else {  // quad_perm [1,0,3,2]: lane xor 1
-    lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false);
-    hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false);
+    lo = dpp_mov<0xB1>(lo);
+    hi = dpp_mov<0xB1>(hi);
   }
   return ((u64)hi << 32) | lo;
 }
