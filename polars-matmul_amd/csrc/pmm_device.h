@@ -107,6 +107,21 @@ __device__ __forceinline__ u64 wave_min_u64(u64 v) {
 // compare per key and one popcount per 64 keys per bit, no LDS: far cheaper
 // than sorting the buffer to find one rank.  The keys of one row are
 // distinct (the corpus index rides in the low bits).
+// The wave-wide reductions' results as scalars (every lane holds the same
+// value; the compiler cannot prove it): the bit loop below then runs on
+// scalar bounds and scalar control flow instead of per-lane copies under
+// exec-mask bookkeeping (8 vector instructions per bit at E = 8, was 15).
+// Round 6, alternated on one box (profiles/r6_merge/kth_uniform_ab.txt):
+// c4 kernel 131.3 / 131.5 -> 130.9 / 130.9 ms (its compactions), merges
+// and c3 unchanged.  Callers run the selection with the whole wave active.
+__device__ __forceinline__ u64 wave_uniform_u64(u64 v) {
+  // (the builtin returns int: through uint32_t, or the low word sign-extends)
+  return ((u64)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+         (u64)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+__device__ __forceinline__ uint32_t wave_uniform_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane(v);
+}
 template <int E>
 __device__ inline u64 wave_kth_u64(const u64 (&x)[E], int k) {
   u64 mx = 0ull, mn = ~0ull;
@@ -115,8 +130,8 @@ __device__ inline u64 wave_kth_u64(const u64 (&x)[E], int k) {
     if (x[e] > mx) mx = x[e];
     if (x[e] != 0ull && x[e] < mn) mn = x[e];
   }
-  mx = wave_max_u64(mx);
-  mn = wave_min_u64(mn);
+  mx = wave_uniform_u64(wave_max_u64(mx));
+  mn = wave_uniform_u64(wave_min_u64(mn));
   if (mx == 0ull) return 0ull;
   const u64 diff = mx ^ mn;
   int b = diff ? 63 - __builtin_clzll(diff) : -1;
@@ -155,6 +170,8 @@ __device__ inline uint32_t wave_kth_u32(const uint32_t (&x)[E], int k) {
     mx = a > mx ? a : mx;
     mn = c < mn ? c : mn;
   }
+  mx = wave_uniform_u32(mx);
+  mn = wave_uniform_u32(mn);
   if (mx == 0u) return 0u;
   const uint32_t diff = mx ^ mn;
   int b = diff ? 31 - __builtin_clz(diff) : -1;
@@ -204,9 +221,10 @@ __device__ __forceinline__ u64 seed_threshold(const u64 (&x)[E], int k) {
 template <int E, typename Store>
 __device__ inline int wave_keep_ge(const u64 (&x)[E], u64 t, Store st, int lane) {
   int base = 0;
+  const u64 t1 = t ? t : 1ull;  // (x >= max(t, 1): x != 0 and x >= t in one compare)
 #pragma unroll
   for (int e = 0; e < E; e++) {
-    const bool keep = x[e] != 0ull && x[e] >= t;
+    const bool keep = x[e] >= t1;
     const u64 m = __ballot(keep);
     if (keep) st(base + lanes_below(m), x[e]);
     base += __popcll(m);
