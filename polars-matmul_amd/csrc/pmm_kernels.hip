@@ -1086,7 +1086,7 @@ __device__ __forceinline__ void merge_row(const MergeArgs &a, const int rpos, co
     return id != 0xFFFFFFFFu ? key : 0ull;
   };
   auto take = [&](u64 x) __attribute__((always_inline)) {
-    const bool keep = (x != 0ull) && (x >= T);
+    const bool keep = x >= (T ? T : 1ull);  // (x != 0 and x >= T in one compare)
     const u64 m = __ballot(keep);
     const int pos = cnt + lanes_below(m);
     if (keep) scr[MP(pos)] = x;
